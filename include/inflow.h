@@ -1,0 +1,136 @@
+/*
+ * inflow.h — C-ABI of libinflow.so, the MI355X (gfx950) implicit-flow density-evaluation engine.
+ *
+ * The reference (musikisomorphie/implicit-normalizing-flows) has no FFI: its hot path is the
+ * PyTorch op sequence inside lib/layers/implicit_block.py.  Each entry point below replaces one
+ * reference call site; the Python drop-in modules (implicit-normalizing-flows_amd/lib/layers)
+ * bind them with ctypes.  Conventions:
+ *   - every pointer is a DEVICE pointer unless documented otherwise; tensors use the reference's
+ *     layout: conv nets NCHW (B, C, H, W) contiguous fp32, fc nets (B, d) row-major fp32;
+ *   - `stream` is a hipStream_t (the caller's current stream); nothing synchronises the device
+ *     except inf_root_find / inf_imblock_forward, which read one residual norm per Broyden
+ *     iteration back to the host exactly where the reference calls .item() (broyden.py:145,157);
+ *   - workspace is caller-allocated (inf_workspace_bytes) so the torch caching allocator owns it;
+ *   - return value 0 = success, otherwise an InfStatus code (inf_status_string()).
+ *   - no global mutable state: calls are re-entrant across streams/threads for distinct workspaces.
+ */
+#ifndef INFLOW_H
+#define INFLOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum InfStatus {
+  INF_OK = 0,
+  INF_ERR_INVALID = 1,     /* bad argument / unsupported net shape */
+  INF_ERR_HIP = 2,         /* a HIP runtime call failed (see inf_last_hip_error) */
+  INF_ERR_WORKSPACE = 3,   /* workspace too small */
+  INF_ERR_UNSUPPORTED = 4  /* layer pattern the engine does not implement */
+} InfStatus;
+
+typedef enum InfLayerKind {
+  INF_LAYER_CONV = 1,    /* InducedNormConv2d  (mixed_lipschitz.py:149-391), stride 1, pad k//2 */
+  INF_LAYER_LINEAR = 2,  /* InducedNormLinear  (mixed_lipschitz.py:12-136) */
+  INF_ACT_SWISH = 3,     /* Swish              (activations.py:64-71) */
+  INF_ACT_SIN = 4        /* Sin                (activations.py:7-12) */
+} InfLayerKind;
+
+typedef struct InfLayerDesc {
+  int kind;                 /* InfLayerKind */
+  int cin, cout, ksize;     /* conv: (cout, cin, k, k) weight; linear: k = 1 */
+  const float* weight;      /* raw (un-normalised) weight, device */
+  const float* bias;        /* (cout) device, or NULL */
+  const float* u;           /* spectral-norm vectors u (codomain) / v (domain), device */
+  const float* v;
+  float coeff;              /* Lipschitz cap: W_eff = W / max(1, u.(W v) / coeff) */
+  const float* beta;        /* Swish beta (1 float) device */
+} InfLayerDesc;
+
+typedef struct InfNetDesc {
+  int n_layers;
+  const InfLayerDesc* layers;   /* host array, nn.Sequential order */
+  int channels, height, width;  /* per-sample input shape; fc nets: channels = d, height = width = 1 */
+} InfNetDesc;
+
+typedef struct InfNet InfNet;   /* opaque: packed, Lipschitz-normalised weights + launch plan */
+
+typedef struct InfBroydenStats {  /* mirrors the dict returned by broyden() (broyden.py:184-193) */
+  int nstep;
+  int lowest_step;
+  int prot_break;         /* 1 => fell back to the Banach fixed point (implicit_block.py:74-75) */
+  int n_trace;
+  double trace[64];       /* ||g||_F per iteration; trace[0] is the initial objective */
+  double diff;            /* ||g(result)||_F */
+  double eps;             /* eps * sqrt(B*d) (broyden.py:131) */
+  int fixed_point_iters;  /* iterations of the fallback, 0 if unused */
+} InfBroydenStats;
+
+/* ---- library ------------------------------------------------------------------------------ */
+int inf_version(void);
+const char* inf_status_string(int status);
+int inf_last_hip_error(void);
+
+/* ---- nets: the nnet_x / nnet_z nn.Sequential of InducedNorm layers + activations ------------ */
+/* Replaces the per-call module walk of nnet(x) (implicit_flow.py:362-399, train_tabular.py:292-311). */
+int inf_net_create(const InfNetDesc* desc, InfNet** out);
+int inf_net_destroy(InfNet* net);
+/* compute_weight(update=False) for every layer (mixed_lipschitz.py:126-132,320-326,378-386):
+ * sigma = u.(W v) on device, W_eff = W / max(1, sigma/coeff), repacked for the MFMA kernels.
+ * Call after any parameter change (the Python side tracks tensor versions). */
+int inf_net_refresh(InfNet* net, void* stream);
+/* Workspace for any call below on a net of this shape at this batch size. */
+size_t inf_workspace_bytes(const InfNet* net, int batch, int threshold);
+/* y = nnet(x). */
+int inf_net_forward(InfNet* net, const float* x, float* y, int batch, void* ws, size_t ws_bytes, void* stream);
+/* out = v^T J_nnet(x)   (one torch.autograd.grad(g, x, v) of implicit_block.py:422). */
+int inf_net_vjp(InfNet* net, const float* x, const float* v, float* out, int batch, void* ws, size_t ws_bytes,
+                void* stream);
+
+/* ---- root finding: RootFind (implicit_block.py:51-100) with broyden (broyden.py:123-193) ------ */
+/* Solve out + f(out) = y + e(y) from out = 0 with Broyden (ls=False); on prot_break fall back to the
+ * Banach iteration from out = y (implicit_block.py:57-65,17-28).  Forward uses (f, e) = (nnet_z, nnet_x);
+ * imBlock.inverse uses (nnet_x, nnet_z) (implicit_block.py:236-243).  diff_detail (device, B floats,
+ * may be NULL) receives the per-sample residual norms of the returned iterate. */
+int inf_root_find(InfNet* net_f, InfNet* net_e, const float* y, float* out, int batch, int threshold, double eps,
+                  InfBroydenStats* stats, float* diff_detail, void* ws, size_t ws_bytes, void* stream);
+/* imBlock forward value: z* = RootFind(nnet_z, nnet_x, x); z = (nnet_x(x) - nnet_z(z*)) + x
+ * (implicit_block.py:226-227). */
+int inf_imblock_forward(InfNet* net_x, InfNet* net_z, const float* x, float* z, int batch, int threshold,
+                        double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- log-det estimators (implicit_block.py:245-350,418-438) --------------------------------- */
+/* out[b] = sum_k coeff[k] * <(J^T)^k vareps_b, vareps_b>,  k = 1..n_terms, coeff[k-1] = (-1)^(k+1)/k * c_k
+ * (coeff is a HOST array, rounded to fp32 as the reference's scalar*tensor product does). */
+int inf_logdet_series(InfNet* net, const float* x, const float* vareps, const float* coeff, int n_terms,
+                      float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* Neumann gradient surrogate value (implicit_block.py:429-438): w = sum_{k=0}^{n} ncoeff[k] (J^T)^k eps,
+ * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
+int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,
+                       float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* Exact log|det(I + J_nnet(x))| for fc nets with d <= 16 (implicit_block.py:249-260,358-362). */
+int inf_logdet_exact(InfNet* net, const float* x, float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- flow glue (elemwise.py:112-128, act_norm.py:153-193, squeeze.py:242-255,
+ *      train_img.py:135-137,543-549) ---------------------------------------------------------- */
+/* y = logit(alpha + (1-2alpha) x); logp_out[b] = logp_in[b] - sum(-log(s - s^2) + log(1-2alpha)). */
+int inf_logit_forward(const float* x, float* y, const float* logp_in, float* logp_out, int batch, int per_sample,
+                      float alpha, void* stream);
+/* y = (x + bias_c) * exp(weight_c); logp_out = logp_in - hw * sum_c weight_c. */
+int inf_actnorm_forward(const float* x, float* y, const float* weight, const float* bias, const float* logp_in,
+                        float* logp_out, int batch, int channels, int hw, void* stream);
+/* space-to-depth by 2: (B,C,H,W) -> (B,4C,H/2,W/2), the reference's permute(0,1,3,5,2,4). */
+int inf_squeeze2(const float* x, float* y, int batch, int channels, int height, int width, void* stream);
+/* out[b] = sum_i (-0.5 log(2 pi) - z_i^2 / 2)  (standard_normal_logprob(z).sum(1)). */
+int inf_normal_logprob(const float* z, float* out, int batch, int per_sample, void* stream);
+/* Rademacher +-1 probes from a counter-based generator (device RNG mode; the reference-replay mode
+ * draws probes on the host, implicit_block.py:297-298). */
+int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INFLOW_H */

@@ -1,0 +1,423 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU (torch fp32, autograd VJPs) restatement of the reference's implicit-flow
+density-evaluation path, written from the reference's behaviour, function by
+function (each cites the reference file:line it follows).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it, and only as the checker / the timed CPU baseline — never as the thing
+measured or shipped.  The product path (``implicit-normalizing-flows_amd``)
+never imports this module.
+
+Pinning: ``tests/golden/make_golden.py`` runs the reference itself (imported in
+the build container with two import shims) on the
+synthetic weights of ``lib/synthetic.py`` and stores its outputs under
+``tests/golden/*.npz``; ``tests/test_oracle_golden.py`` checks this oracle
+against those vectors.
+
+Inputs are (arch, state_dict) pairs from ``lib/synthetic.py``: state dicts keyed
+exactly like the reference models.  RNG consumption replays the reference: per
+power-series block ``np.random.poisson|geometric(.., 1)`` from numpy's global RNG,
+then ``vareps_x`` then ``vareps_z`` Rademacher from torch's global CPU generator
+(implicit_block.py:262-298).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------------------
+# Lipschitz-normalised layers (eval: compute_weight(update=False))
+# ---------------------------------------------------------------------------------------
+
+
+def induced_norm_weight(sd, key, coeff):
+    """W / max(1, sigma/coeff) with sigma = u . (W v)   (mixed_lipschitz.py:126-132 linear,
+    :320-326 1x1 conv, :378-386 kxk conv)."""
+    W = sd[key + '.weight']
+    u, v = sd[key + '.u'], sd[key + '.v']
+    if W.dim() == 2:
+        sigma = torch.dot(u, torch.mv(W, v))
+    elif W.shape[-1] == 1:
+        Wm = W.view(W.shape[0], W.shape[1])
+        sigma = torch.dot(u, torch.mv(Wm, v))
+    else:
+        h, w = [int(t) for t in sd[key + '.spatial_dims'].tolist()]
+        k = W.shape[-1]
+        wv = F.conv2d(v.view(1, W.shape[1], h, w), W, stride=1, padding=k // 2, bias=None).view(-1)
+        sigma = torch.dot(u.view(-1), wv)
+    factor = torch.max(torch.ones(1), sigma / coeff)
+    return W / factor
+
+
+def swish(x, beta):
+    """activations.py:70-71:  x * sigmoid(x * softplus(beta)) / 1.1"""
+    return (x * torch.sigmoid(x * F.softplus(beta))) / 1.1
+
+
+def sin_act(x):
+    """activations.py:11-12:  sin(2 pi x) / pi * 0.5"""
+    return torch.sin(2. * math.pi * x) / math.pi * 0.5
+
+
+def make_net(sd, prefix, layout_net, coeff):
+    """Functional nnet: the nn.Sequential of InducedNormConv2d/Linear + activations
+    (implicit_flow.py:362-399 conv nets, train_tabular.py:292-311 fc nets)."""
+    ops = []
+    for j, layer in enumerate(layout_net):
+        key = '%s.%d' % (prefix, j)
+        if layer[0] == 'conv':
+            W = induced_norm_weight(sd, key, coeff)
+            ops.append(('conv', W, sd[key + '.bias'], layer[3] // 2))
+        elif layer[0] == 'linear':
+            ops.append(('linear', induced_norm_weight(sd, key, coeff), sd[key + '.bias']))
+        elif layer[0] == 'swish':
+            ops.append(('swish', sd[key + '.beta']))
+        elif layer[0] == 'sin':
+            ops.append(('sin',))
+        else:
+            raise ValueError(layer)
+
+    def net(x):
+        for op in ops:
+            if op[0] == 'conv':
+                x = F.conv2d(x, op[1], op[2], 1, op[3], 1, 1)   # mixed_lipschitz.py:391
+            elif op[0] == 'linear':
+                x = F.linear(x, op[1], op[2])                      # mixed_lipschitz.py:136
+            elif op[0] == 'swish':
+                x = swish(x, op[1])
+            else:
+                x = sin_act(x)
+        return x
+    return net
+
+
+# ---------------------------------------------------------------------------------------
+# Broyden (broyden.py:101-193, ls=False) and Banach fixed point (implicit_block.py:17-28)
+# ---------------------------------------------------------------------------------------
+
+
+def _rmatvec(Us, VTs, x):
+    """broyden.py:101-109:  x^T(-I + U V^T)"""
+    if Us.nelement() == 0:
+        return -x
+    xTU = torch.einsum('bi, bij -> bj', x, Us)
+    return -x + torch.einsum('bj, bji -> bi', xTU, VTs)
+
+
+def _matvec(Us, VTs, x):
+    """broyden.py:112-120:  (-I + U V^T) x"""
+    if Us.nelement() == 0:
+        return -x
+    VTx = torch.einsum('bji, bi -> bj', VTs, x)
+    return -x + torch.einsum('bij, bj -> bi', Us, VTx)
+
+
+def broyden(g_, x0, threshold, eps):
+    """Good-Broyden inverse-Jacobian root solve, line search off (broyden.py:123-193,
+    line_search(on=False) = broyden.py:66-99 with s = 1)."""
+    shape = x0.shape
+    x0 = x0.view(shape[0], -1)
+    bsz, d = x0.size()
+    eps = eps * np.sqrt(np.prod(x0.shape))                       # :131
+
+    def g(x):
+        return g_(x.view(shape)).view(bsz, -1)
+
+    x_est = x0
+    gx = g(x_est)
+    nstep = 0
+    Us = torch.zeros(bsz, d, threshold)
+    VTs = torch.zeros(bsz, threshold, d)
+    update = -gx                                                  # :144
+    new_objective = init_objective = torch.norm(gx).item()
+    prot_break = False
+    trace = [init_objective]
+    lowest = new_objective
+    lowest_xest, lowest_gx, lowest_step = x_est, gx, nstep
+    while new_objective >= eps and nstep < threshold:             # :153
+        x_new = x_est + update                                    # line_search(on=False), :94-99
+        gx_new = g(x_new)
+        delta_x, delta_gx = x_new - x_est, gx_new - gx
+        x_est, gx = x_new, gx_new
+        nstep += 1
+        new_objective = torch.norm(gx).item()
+        trace.append(new_objective)
+        if new_objective < lowest:                                # :159-162
+            lowest_xest, lowest_gx = x_est.clone(), gx.clone()
+            lowest = new_objective
+            lowest_step = nstep
+        if new_objective < eps:
+            break
+        if new_objective < 3 * eps and nstep == threshold and \
+                np.max(trace[-threshold:]) / np.min(trace[-threshold:]) < 1.3:   # :165-168
+            break
+        if new_objective > init_objective * 1e6:                  # :169-172
+            prot_break = True
+            break
+        m = (nstep - 1) % threshold
+        part_Us, part_VTs = Us[:, :, :m], VTs[:, :m]
+        vT = _rmatvec(part_Us, part_VTs, delta_x)                 # :175
+        u = (delta_x - _matvec(part_Us, part_VTs, delta_gx)) / torch.einsum('bi, bi -> b', vT, delta_gx)[:, None]
+        vT[vT != vT] = 0                                          # :177-178
+        u[u != u] = 0
+        VTs[:, m] = vT
+        Us[:, :, m] = u
+        update = -_matvec(Us[:, :, :nstep], VTs[:, :nstep], gx)   # :181
+    return {"result": lowest_xest.view(shape), "nstep": nstep, "lowest_step": lowest_step,
+            "diff": torch.norm(lowest_gx).item(), "diff_detail": torch.norm(lowest_gx, dim=1),
+            "prot_break": prot_break, "trace": trace, "eps": eps, "threshold": threshold}
+
+
+def find_fixed_point(g, y, threshold=1000, eps=1e-5):
+    """implicit_block.py:17-28"""
+    x, x_prev = g(y), y
+    i = 0
+    tol = eps + eps * y.abs()
+    while not torch.all((x - x_prev) ** 2 / tol < 1.):
+        x, x_prev = g(x), x
+        i += 1
+        if i > threshold:
+            break
+    return x
+
+
+def root_find(fz, fx, z0, x, eps, threshold):
+    """RootFind.broyden_find_root (implicit_block.py:68-80) with the prot_break fallback
+    to banach_find_root (:57-65)."""
+    with torch.no_grad():
+        x_embed = fx(x) + x
+        info = broyden(lambda z: x_embed - fz(z) - z, torch.zeros_like(z0), threshold, eps)
+        if info['prot_break']:
+            z_est = find_fixed_point(lambda z: x_embed - fz(z), z0, threshold=1000, eps=eps)
+        else:
+            z_est = info['result']
+    return z_est.clone().detach(), info
+
+
+# ---------------------------------------------------------------------------------------
+# Log-det estimators (implicit_block.py:245-350, 358-366, 418-438, 457-483)
+# ---------------------------------------------------------------------------------------
+
+
+def geometric_1mcdf(p, k, offset):
+    """implicit_block.py:461-467"""
+    if k <= offset:
+        return 1.
+    k = k - offset
+    return (1 - p) ** max(k - 1, 0)
+
+
+def poisson_1mcdf(lamb, k, offset):
+    """implicit_block.py:474-483"""
+    if k <= offset:
+        return 1.
+    k = k - offset
+    s = 1.
+    for i in range(1, k):
+        s += lamb ** i / math.factorial(i)
+    return 1 - np.exp(-lamb) * s
+
+
+def series_plan(n_dist, lamb, geom_logit, n_exact, n_samples=1):
+    """Draw the series length and return (n_power_series, coeff_fn, n_samples)
+    (implicit_block.py:261-289; numpy global RNG, one draw per call)."""
+    if n_dist == 'geometric':
+        geom_p = float(torch.sigmoid(torch.tensor(geom_logit)).float().item())
+        ns = np.random.geometric(geom_p, n_samples)
+        rcdf = lambda k, off: geometric_1mcdf(geom_p, k, off)
+    else:
+        ns = np.random.poisson(lamb, n_samples)
+        rcdf = lambda k, off: poisson_1mcdf(lamb, k, off)
+    n_ps = max(ns) + n_exact
+    coeff_fn = lambda k: 1 / rcdf(k, n_exact) * sum(ns >= k - n_exact) / len(ns)
+    return n_ps, coeff_fn, ns
+
+
+def rademacher_like(x):
+    """implicit_block.py:297-298 (torch CPU generator; Bernoulli(0.5).sample(shape))."""
+    return torch.distributions.bernoulli.Bernoulli(torch.Tensor([0.5])).sample(x.shape).reshape(x.shape) * 2 - 1
+
+
+def basic_logdet_estimator(g, x, n_power_series, vareps, coeff_fn):
+    """implicit_block.py:418-426 (eval: create_graph=False)"""
+    vjp = vareps
+    logdetgrad = torch.tensor(0.)
+    for k in range(1, n_power_series + 1):
+        vjp = torch.autograd.grad(g, x, vjp, retain_graph=True)[0]
+        tr = torch.sum(vjp.view(x.shape[0], -1) * vareps.view(x.shape[0], -1), 1)
+        delta = (-1) ** (k + 1) / k * coeff_fn(k) * tr
+        logdetgrad = logdetgrad + delta
+    return logdetgrad
+
+
+def neumann_logdet_estimator(g, x, n_power_series, vareps, coeff_fn):
+    """implicit_block.py:429-438 (forward value only; a gradient surrogate, README.md:33)"""
+    vjp = vareps
+    neumann_vjp = vareps
+    with torch.no_grad():
+        for k in range(1, n_power_series + 1):
+            vjp = torch.autograd.grad(g, x, vjp, retain_graph=True)[0]
+            neumann_vjp = neumann_vjp + (-1) ** k * coeff_fn(k) * vjp
+    vjp_jac = torch.autograd.grad(g, x, neumann_vjp)[0]
+    return torch.sum(vjp_jac.view(x.shape[0], -1) * vareps.view(x.shape[0], -1), 1)
+
+
+def batch_jacobian(g, x):
+    """implicit_block.py:358-362"""
+    jac = []
+    for d in range(g.shape[1]):
+        jac.append(torch.autograd.grad(torch.sum(g[:, d]), x, retain_graph=True)[0].view(x.shape[0], 1, x.shape[1]))
+    return torch.cat(jac, 1)
+
+
+class ImBlock:
+    """imBlock eval semantics (implicit_block.py:103-162 ctor defaults, 220-234 forward,
+    245-350 _logdetgrad)."""
+
+    def __init__(self, sd, prefix, layout_net, arch, training=False):
+        self.fx = make_net(sd, prefix + '.nnet_x', layout_net, arch['coeff'])
+        self.fz = make_net(sd, prefix + '.nnet_z', layout_net, arch['coeff'])
+        self.lamb = float(sd[prefix + '.lamb'])
+        self.geom_logit = float(np.log(arch['geom_p']) - np.log(1. - arch['geom_p']))
+        self.arch = arch
+        self.training = training
+        self.brute_force = arch.get('brute_force', False)
+        self.eps_forward = arch['eps_forward']
+        self.threshold = arch['threshold']
+        self.record = {}
+
+    def logdetgrad(self, z, x, estimator='basic'):
+        a = self.arch
+        with torch.enable_grad():
+            if (self.brute_force or not self.training) and (x.ndimension() == 2 and x.shape[1] <= 10):
+                x = x.detach().requires_grad_(True)
+                z = z.detach().requires_grad_(True)
+                Jx = batch_jacobian(x + self.fx(x), x)
+                Jz = batch_jacobian(z + self.fz(z), z)
+                return (torch.logdet(Jx) - torch.logdet(Jz)).view(-1, 1).detach()
+            n_exact = a['n_exact_terms'] if self.training else a['n_exact_terms_test']
+            n_ps, coeff_fn, ns = series_plan(a['n_dist'], self.lamb, self.geom_logit, n_exact)
+            self.record['n_power_series'] = int(n_ps)
+            vareps_x = rademacher_like(x)
+            vareps_z = rademacher_like(z)
+            est = basic_logdet_estimator if estimator == 'basic' else neumann_logdet_estimator
+            x = x.detach().requires_grad_(True)
+            z = z.detach().requires_grad_(True)
+            ldx = est(self.fx(x), x, n_ps, vareps_x, coeff_fn)
+            ldz = est(self.fz(z), z, n_ps, vareps_z, coeff_fn)
+            return (ldx - ldz).view(-1, 1).detach()
+
+    def forward(self, x, logpx=None):
+        z0 = x.clone().detach()
+        z_star, info = root_find(self.fz, self.fx, z0, z0, self.eps_forward, self.threshold)
+        self.record.update(nstep=info['nstep'], lowest_step=info['lowest_step'],
+                           prot_break=info['prot_break'], trace=info['trace'])
+        with torch.no_grad():
+            z = (self.fx(z0) - self.fz(z_star)) + z0                 # :227
+        if logpx is None:
+            return z
+        return z, logpx - self.logdetgrad(z, x)
+
+
+# ---------------------------------------------------------------------------------------
+# Flow glue (elemwise.py:112-128, act_norm.py:153-193, squeeze.py:242-255)
+# ---------------------------------------------------------------------------------------
+
+
+def logit_forward(x, logpx, alpha):
+    s = alpha + (1 - 2 * alpha) * x
+    y = torch.log(s) - torch.log(1 - s)
+    ld = -torch.log(s - s * s) + math.log(1 - 2 * alpha)
+    return y, logpx - ld.view(x.size(0), -1).sum(1, keepdim=True)
+
+
+def actnorm_forward(x, logpx, w, b):
+    shape = [1, -1, 1, 1] if x.dim() == 4 else [1, -1]
+    y = (x + b.view(*shape).expand_as(x)) * torch.exp(w.view(*shape).expand_as(x))
+    ld = w.view(*shape).expand(*x.size()).contiguous().view(x.size(0), -1).sum(1, keepdim=True)
+    return y, logpx - ld
+
+
+def squeeze2(x):
+    B, c, h, w = x.shape
+    return x.reshape(B, c, h // 2, 2, w // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, c * 4, h // 2, w // 2)
+
+
+class ConvFlow:
+    """ImplicitFlow(factor_out=False, fc_end=False) eval forward (implicit_flow.py:189-219)."""
+
+    def __init__(self, arch, sd, layout):
+        self.arch = arch
+        self.steps = []
+        for i, chain in enumerate(layout):
+            for j, (kind, info) in enumerate(chain):
+                p = 'transforms.%d.chain.%d' % (i, j)
+                if kind == 'imblock':
+                    self.steps.append(('imblock', ImBlock(sd, p, info['net'], arch)))
+                elif kind == 'actnorm':
+                    self.steps.append(('actnorm', (sd[p + '.weight'], sd[p + '.bias'])))
+                else:
+                    self.steps.append((kind, info))
+
+    def forward(self, x, logpx):
+        for kind, obj in self.steps:
+            if kind == 'imblock':
+                x, logpx = obj.forward(x, logpx)
+            elif kind == 'actnorm':
+                x, logpx = actnorm_forward(x, logpx, *obj)
+            elif kind == 'logit':
+                x, logpx = logit_forward(x, logpx, obj['alpha'])
+            else:
+                x = squeeze2(x)
+        return x.view(x.size(0), -1), logpx
+
+    def blocks(self):
+        return [o for k, o in self.steps if k == 'imblock']
+
+
+class FCFlow:
+    """SequentialFlow([imBlock] * n) (container.py:12-20; train_tabular.py:314-336)."""
+
+    def __init__(self, arch, sd, layout, training=False):
+        self.blk = [ImBlock(sd, 'chain.%d' % j, info['net'], arch, training) for j, (k, info) in enumerate(layout)]
+
+    def forward(self, x, logpx):
+        for b in self.blk:
+            x, logpx = b.forward(x, logpx)
+        return x, logpx
+
+    def blocks(self):
+        return self.blk
+
+
+def standard_normal_logprob(z):
+    """train_img.py:135-137"""
+    return -0.5 * math.log(2 * math.pi) - z.pow(2) / 2
+
+
+def image_bits_per_dim(flow, x, nvals=256):
+    """compute_loss density branch (train_img.py:517-554) with padding 0: returns
+    (bpd, logpx per sample, z)."""
+    with torch.no_grad():
+        z, delta_logp = flow.forward(x, 0)
+    logpz = standard_normal_logprob(z).view(z.size(0), -1).sum(1, keepdim=True)
+    ndim = x[0].numel()
+    logpx = logpz - delta_logp - np.log(nvals) * ndim - torch.zeros(x.shape[0], 1)
+    bpd = -torch.mean(logpx) / ndim / np.log(2)
+    return bpd, logpx, z
+
+
+def tabular_nats(flow, x):
+    """compute_loss (train_tabular.py:398-410 / train_toy.py:103-119): (loss, logpx, z)."""
+    with torch.no_grad():
+        z, delta_logp = flow.forward(x, torch.zeros(x.shape[0], 1))
+    logpz = standard_normal_logprob(z).sum(1, keepdim=True)
+    logpx = logpz - delta_logp
+    return -torch.mean(logpx), logpx, z
+
+
+def build(arch, sd, layout, training=False):
+    if arch['kind'] == 'conv':
+        return ConvFlow(arch, sd, layout)
+    return FCFlow(arch, sd, layout, training)
