@@ -1,0 +1,815 @@
+// Host side of libinflow: net plans, the forward / VJP launch chains, the Broyden driver,
+// the log-det estimators and the C-ABI of include/inflow.h.
+//
+// Reference mapping (all implicit_block.py unless noted):
+//   inf_net_refresh       <- InducedNorm*.compute_weight(update=False) (mixed_lipschitz.py:126-132,267-386)
+//   inf_net_forward       <- nnet(x)                      (nn.Sequential of InducedNorm + Swish/Sin)
+//   inf_net_vjp           <- torch.autograd.grad(g, x, v)                                   (:422)
+//   inf_root_find         <- RootFind.apply -> broyden_find_root -> broyden              (:51-100)
+//   inf_imblock_forward   <- imBlock.forward value path                                  (:220-230)
+//   inf_logdet_series     <- basic_logdet_estimator                                      (:418-426)
+//   inf_logdet_neumann    <- neumann_logdet_estimator                                    (:429-438)
+//   inf_logdet_exact      <- brute-force batch_jacobian + torch.logdet                   (:249-260)
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "glue.h"
+#include "kernels.h"
+
+namespace inf {
+static thread_local int g_last_hip = 0;
+void set_hip_error(hipError_t e) { g_last_hip = (int)e; }
+}  // namespace inf
+
+using namespace inf;
+
+namespace {
+
+constexpr int TAPS_MAX_CH = 64;   // 3x3 convs with fewer output channels than this use packed taps
+constexpr int SERIES_MAX = 128;
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+struct Operand {
+  int load = BL_DIRECT;  // B-operand loader
+  int taps = 0;          // output is packed taps (3x3, small M) -> conv_out sums 9 shifts
+  int M = 0, Mpad = 0, K = 0, Kpad = 0;
+  int pack = PK_ROWMAJOR;
+  float* A = nullptr;
+};
+
+struct WLayer {
+  int kind = 0, cin = 0, cout = 0, ks = 1;
+  const float *W = nullptr, *b = nullptr, *u = nullptr, *v = nullptr;
+  float coeff = 1.f;
+  int act = ACT_NONE;             // activation applied to this layer's output
+  const float* act_beta = nullptr;
+  Operand f, g;                   // forward, vjp
+  float* factor = nullptr;        // device [factor, sigma]
+};
+
+}  // namespace
+
+struct InfNet {
+  int C = 0, H = 1, W = 1, P = 1, d = 0;
+  bool fc = false;
+  int pre_act = ACT_NONE;
+  const float* pre_beta = nullptr;
+  std::vector<WLayer> L;
+  int hidden_max = 0;      // channels of the widest intermediate activation
+  int rows_max = 0;        // rows of the widest output-stage buffer Y
+  float* dev = nullptr;    // packed operands + factors (owned)
+  double* scratch = nullptr;
+  size_t scratch_doubles = 0;
+  int device = 0;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// workspace carving
+// ---------------------------------------------------------------------------------------------
+struct WS {
+  char* base;
+  size_t cap, off;
+  bool ok = true;
+  template <typename T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    if (off > cap) ok = false;
+    return p;
+  }
+};
+
+struct Bufs {
+  float *h0, *h1, *Y;
+  std::vector<float*> D;   // saved activation derivatives, one per hidden layer
+  float *xin, *xemb, *fx, *xa, *xb, *ga, *gb, *upd, *dx, *dg, *lowest, *va, *vb, *eps_t, *zero, *tmp;
+  float *U, *VT;
+  float *ext0, *ext1;
+  double *part, *bpart, *sumsq;
+  unsigned int* counter;
+  int nchunk;
+};
+
+size_t per_sample_hidden(const InfNet* n) { return (size_t)n->hidden_max * (n->fc ? 1 : n->P); }
+
+// layout-aware sizes: E = B * d elements per vector
+// Carves the workspace; returns the bytes required (fits iff result <= cap).  With ws == nullptr it
+// only measures.
+size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
+  WS w{reinterpret_cast<char*>(ws), cap, 0};
+  const size_t E = (size_t)B * n->d;
+  const size_t Hs = (size_t)B * per_sample_hidden(n);
+  const size_t Ys = (size_t)B * n->rows_max * (n->fc ? 1 : n->P);
+  const int nchunk = n->fc ? 1 : out_nchunk(n->d);
+  b.nchunk = nchunk;
+  b.h0 = w.take<float>(Hs);
+  b.h1 = w.take<float>(Hs);
+  b.Y = w.take<float>(Ys);
+  b.D.resize(n->L.size() > 0 ? n->L.size() - 1 : 0);
+  for (auto& p : b.D) p = w.take<float>(Hs);
+  float** vecs[] = {&b.xin, &b.xemb, &b.fx, &b.xa, &b.xb, &b.ga, &b.gb, &b.upd,
+                    &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp};
+  for (float** v : vecs) *v = w.take<float>(E);
+  b.U = w.take<float>((size_t)T * E);
+  b.VT = w.take<float>((size_t)T * E);
+  if (n->fc) {
+    const size_t ext = (size_t)(n->d + 1) * B * std::max(n->hidden_max, n->d);
+    b.ext0 = w.take<float>(ext);
+    b.ext1 = w.take<float>(ext);
+  } else {
+    b.ext0 = b.ext1 = nullptr;
+  }
+  b.part = w.take<double>((size_t)B * nchunk * SERIES_MAX);
+  const int bch = (n->d + 1023) / 1024;
+  b.bpart = w.take<double>((size_t)B * bch * (3 * (size_t)T + 2) + 64);
+  b.sumsq = w.take<double>((size_t)B);
+  b.counter = w.take<unsigned int>(64);
+  return w.off + 256;
+}
+
+size_t ws_need(const InfNet* n, int B, int T) {
+  Bufs b;
+  return carve(n, B, T, nullptr, 0, b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// GEMM argument builders
+// ---------------------------------------------------------------------------------------------
+GemmArgs gemm_base(const InfNet* n, const Operand& op, const float* X, int in_ch, int B) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.A = op.A;
+  g.M = op.M;
+  g.Kpad = op.Kpad;
+  g.Ktot = op.K;
+  g.X = X;
+  if (n->fc) {        // feature-major (ch, B): one "image" with B pixels
+    g.P = B;
+    g.N = B;
+    g.x_sample = 0;
+    g.H = 1;
+    g.W = B;
+  } else {
+    g.P = n->P;
+    g.N = B * n->P;
+    g.x_sample = (long)in_ch * n->P;
+    g.H = n->H;
+    g.W = n->W;
+  }
+  return g;
+}
+
+void set_out(const InfNet* n, GemmArgs& g, float* out, int out_rows) {
+  g.out = out;
+  g.o_sample = n->fc ? 0 : (long)out_rows * n->P;
+}
+
+// Forward chain.  mode = OM_* for the output stage, or -1 for "save derivatives only" (log-det prep:
+// the last layer is skipped, D[l] = act'(a_l) are kept).  x is in internal layout.
+int run_forward(InfNet* n, const float* x, int B, Bufs& bf, int mode, const OutArgs* oa, hipStream_t s) {
+  const int L = (int)n->L.size();
+  const float* cur = x;
+  int cur_ch = n->C;
+  for (int l = 0; l < L - 1; ++l) {
+    const WLayer& w = n->L[l];
+    float* out = (l % 2 == 0) ? bf.h0 : bf.h1;
+    GemmArgs g = gemm_base(n, w.f, cur, cur_ch, B);
+    g.pre_beta = (l == 0) ? n->pre_beta : nullptr;
+    set_out(n, g, out, w.cout);
+    g.bias = w.b;
+    g.act = w.act;
+    g.act_beta = w.act_beta;
+    g.deriv_out = (mode < 0) ? bf.D[l] : nullptr;
+    g.write_out = (mode < 0 && l == L - 2) ? 0 : 1;
+    INF_TRY(launch_gemm(g, w.f.load, EP_BIAS_ACT, s));
+    cur = out;
+    cur_ch = w.cout;
+  }
+  if (mode < 0) return INF_OK;
+  const WLayer& w = n->L[L - 1];
+  GemmArgs g = gemm_base(n, w.f, cur, cur_ch, B);
+  g.pre_beta = (L == 1) ? n->pre_beta : nullptr;
+  set_out(n, g, bf.Y, w.f.M);
+  INF_TRY(launch_gemm(g, w.f.load, EP_STORE, s));
+  OutArgs a = *oa;
+  a.Y = bf.Y;
+  a.y_sample = n->fc ? 0 : (long)w.f.M * n->P;
+  a.C = n->C;
+  a.H = n->H;
+  a.W = n->W;
+  a.ks = w.f.taps ? 3 : 1;
+  a.mode = mode;
+  a.bias = w.b;
+  a.pre_beta = nullptr;
+  return n->fc ? launch_fc_out(a, B, s) : launch_conv_out(a, B, s);
+}
+
+// One VJP: vout = v^T J(x), using D saved by run_forward(mode=-1) on x.  partial (B x nchunk doubles,
+// may be null) receives the per-sample partial sums of vout . eps.
+int run_vjp(InfNet* n, const float* v, float* vout, const float* xin, const float* eps, double* partial, int B,
+            Bufs& bf, hipStream_t s) {
+  const int L = (int)n->L.size();
+  const float* cur = v;
+  int cur_ch = n->C;
+  for (int l = L - 1; l >= 1; --l) {
+    const WLayer& w = n->L[l];
+    float* out = ((L - 1 - l) % 2 == 0) ? bf.h0 : bf.h1;
+    GemmArgs g = gemm_base(n, w.g, cur, cur_ch, B);
+    set_out(n, g, out, w.cin);
+    g.deriv_in = bf.D[l - 1];
+    INF_TRY(launch_gemm(g, w.g.load, EP_MUL_DERIV, s));
+    cur = out;
+    cur_ch = w.cin;
+  }
+  const WLayer& w = n->L[0];
+  GemmArgs g = gemm_base(n, w.g, cur, cur_ch, B);
+  set_out(n, g, bf.Y, w.g.M);
+  INF_TRY(launch_gemm(g, w.g.load, EP_STORE, s));
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.Y = bf.Y;
+  a.y_sample = n->fc ? 0 : (long)w.g.M * n->P;
+  a.C = n->C;
+  a.H = n->H;
+  a.W = n->W;
+  a.ks = w.g.taps ? 3 : 1;
+  a.mode = OM_VJP;
+  a.in0 = eps;
+  a.in1 = xin;
+  a.out0 = vout;
+  a.pre_beta = n->pre_beta;
+  a.partial = partial;
+  a.nchunk = n->fc ? 1 : out_nchunk(n->d);
+  return n->fc ? launch_fc_out(a, B, s) : launch_conv_out(a, B, s);
+}
+
+// residual evaluation g = x_embed - f(z) - z (+ dg = g - g_prev) and per-sample sum of squares -> host
+// zsub is the subtracted "- z" term: z itself for Broyden, zeros for the Banach map x_embed - f(z).
+int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
+               const float* gprev, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = xemb;
+  a.in1 = zsub;
+  a.in2 = gprev;
+  a.out0 = gout;
+  a.out1 = dg;
+  a.partial = bf.part;
+  a.nchunk = bf.nchunk;
+  INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
+  if (f->fc) {
+    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  } else {
+    INF_TRY(launch_reduce_partials(bf.part, B, bf.nchunk, bf.sumsq, s));
+    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  }
+  INF_HIP(hipStreamSynchronize(s));
+  return INF_OK;
+}
+
+double total(const std::vector<double>& v) {
+  double t = 0.0;
+  for (double x : v) t += x;
+  return t;
+}
+
+// x (boundary layout) -> internal layout buffer
+const float* to_internal(InfNet* n, const float* x, float* buf, int B, hipStream_t s, int* st) {
+  if (!n->fc) return x;
+  *st = launch_transpose(x, buf, B, n->d, s);
+  return buf;
+}
+int to_boundary(InfNet* n, const float* xi, float* out, int B, hipStream_t s) {
+  if (!n->fc) {
+    if (xi != out) INF_HIP(hipMemcpyAsync(out, xi, sizeof(float) * (size_t)B * n->d, hipMemcpyDeviceToDevice, s));
+    return INF_OK;
+  }
+  return launch_transpose(xi, out, n->d, B, s);
+}
+
+bool same_shape(const InfNet* a, const InfNet* b) {
+  return a->C == b->C && a->H == b->H && a->W == b->W && a->fc == b->fc && a->d == b->d;
+}
+
+// Broyden root find on internal-layout buffers.  Solves z with g(z) = xemb - f(z) - z = 0.
+// Result (lowest iterate) in bf.lowest.  y (internal) is the Banach fallback start.
+int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
+                  Bufs& bf, hipStream_t s) {
+  const size_t E = (size_t)B * f->d;
+  const long cs = (long)E;
+  const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
+  std::vector<double> ss(B), lowest_ss(B);
+  const double eps = eps_in * sqrt((double)E);                       // broyden.py:131
+  InfBroydenStats stats;
+  memset(&stats, 0, sizeof(stats));
+  stats.eps = eps;
+
+  float *x = bf.xa, *xn = bf.xb, *gx = bf.ga, *gn = bf.gb;
+  INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
+  INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
+  INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
+  INF_TRY(eval_resid(f, x, x, bf.xemb, gx, nullptr, nullptr, B, bf, ss, s));
+  const double init = sqrt(total(ss));
+  double obj = init, lowest = init;
+  lowest_ss = ss;
+  int nstep = 0, lowest_step = 0;
+  std::vector<double> trace{init};
+  INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  // update = -gx; x_est = x0 + update
+  INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
+  INF_TRY(launch_axpy_step(x, bf.upd, xn, bf.dx, (long)E, s));
+  while (obj >= eps && nstep < T) {                                   // broyden.py:153
+    INF_TRY(eval_resid(f, xn, xn, bf.xemb, gn, bf.dg, gx, B, bf, ss, s));
+    std::swap(x, xn);
+    std::swap(gx, gn);
+    nstep += 1;
+    obj = sqrt(total(ss));
+    trace.push_back(obj);
+    if (obj < lowest) {                                               // :159-162
+      INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+      lowest = obj;
+      lowest_step = nstep;
+      lowest_ss = ss;
+    }
+    if (obj < eps) break;
+    if (obj < 3 * eps && nstep == T) {                                // :165-168
+      const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
+      double mx = trace[k0], mn = trace[k0];
+      for (size_t k = k0; k < trace.size(); ++k) {
+        mx = std::max(mx, trace[k]);
+        mn = std::min(mn, trace[k]);
+      }
+      if (mx / mn < 1.3) break;
+    }
+    if (obj > init * 1e6) {                                           // :169-172
+      stats.prot_break = 1;
+      break;
+    }
+    BroydenArgs ba;
+    memset(&ba, 0, sizeof(ba));
+    ba.batch = B;
+    ba.d = f->d;
+    ba.T = T;
+    ba.sb = sb;
+    ba.si = si;
+    ba.cs = cs;
+    ba.U = bf.U;
+    ba.VT = bf.VT;
+    ba.dx = bf.dx;
+    ba.dg = bf.dg;
+    ba.gx = gx;
+    ba.x = x;
+    ba.xnew = xn;
+    ba.dxnew = bf.dx;
+    ba.upd = bf.upd;
+    ba.part = bf.bpart;
+    ba.m = (nstep - 1) % T;
+    ba.ncols = std::min(nstep, T);
+    INF_TRY(launch_broyden_update(ba, s));
+  }
+  stats.nstep = nstep;
+  stats.lowest_step = lowest_step;
+  stats.diff = lowest;
+  stats.n_trace = (int)std::min<size_t>(trace.size(), 64);
+  for (int k = 0; k < stats.n_trace; ++k) stats.trace[k] = trace[k];
+  if (diff_detail) {
+    std::vector<float> dd(B);
+    for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
+    INF_HIP(hipMemcpyAsync(diff_detail, dd.data(), sizeof(float) * B, hipMemcpyHostToDevice, s));
+    INF_HIP(hipStreamSynchronize(s));
+  }
+  if (stats.prot_break) {
+    // banach_find_root (implicit_block.py:57-65): z <- x_embed - f(z) from z0 = y, <= 1000 iterations
+    float *zc = bf.xa, *zn = bf.xb;
+    INF_HIP(hipMemsetAsync(bf.zero, 0, sizeof(float) * E, s));
+    INF_HIP(hipMemcpyAsync(zc, y, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+    std::vector<double> dummy(B);
+    int it = 0;
+    // x = g(y)
+    INF_TRY(eval_resid(f, zc, bf.zero, bf.xemb, zn, nullptr, nullptr, B, bf, dummy, s));
+    std::swap(zc, zn);   // zc = x, zn = x_prev (= y)
+    INF_HIP(hipMemcpyAsync(zn, y, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+    for (;;) {
+      unsigned int bad = 0;
+      INF_HIP(hipMemsetAsync(bf.counter, 0, sizeof(unsigned int), s));
+      INF_TRY(glue_fixed_point_check(zc, zn, y, (long)E, (float)eps_in, bf.counter, s));
+      INF_HIP(hipMemcpyAsync(&bad, bf.counter, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+      INF_HIP(hipStreamSynchronize(s));
+      if (bad == 0) break;
+      INF_TRY(eval_resid(f, zc, bf.zero, bf.xemb, zn, nullptr, nullptr, B, bf, dummy, s));
+      std::swap(zc, zn);
+      it += 1;
+      if (it > 1000) break;
+    }
+    INF_HIP(hipMemcpyAsync(bf.lowest, zc, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+    stats.fixed_point_iters = it;
+  }
+  if (st) *st = stats;
+  return INF_OK;
+}
+
+}  // namespace
+
+// ==============================================================================================
+// C-ABI
+// ==============================================================================================
+extern "C" {
+
+int inf_version(void) { return 1; }
+
+const char* inf_status_string(int s) {
+  switch (s) {
+    case INF_OK: return "ok";
+    case INF_ERR_INVALID: return "invalid argument";
+    case INF_ERR_HIP: return "HIP runtime error";
+    case INF_ERR_WORKSPACE: return "workspace too small";
+    case INF_ERR_UNSUPPORTED: return "unsupported net layout";
+    default: return "unknown status";
+  }
+}
+
+int inf_last_hip_error(void) { return inf::g_last_hip; }
+
+int inf_net_create(const InfNetDesc* desc, InfNet** out) {
+  if (!desc || !out || desc->n_layers <= 0 || !desc->layers) return INF_ERR_INVALID;
+  InfNet* n = new (std::nothrow) InfNet();
+  if (!n) return INF_ERR_INVALID;
+  n->C = desc->channels;
+  n->H = desc->height;
+  n->W = desc->width;
+  n->P = n->H * n->W;
+  n->d = n->C * n->P;
+  int i = 0;
+  // leading activation (preact, implicit_flow.py:371-373)
+  if (desc->layers[0].kind == INF_ACT_SWISH || desc->layers[0].kind == INF_ACT_SIN) {
+    n->pre_act = desc->layers[0].kind == INF_ACT_SWISH ? ACT_SWISH : ACT_SIN;
+    n->pre_beta = desc->layers[0].beta;
+    if (n->pre_act != ACT_SWISH) { delete n; return INF_ERR_UNSUPPORTED; }
+    i = 1;
+  }
+  for (; i < desc->n_layers; ++i) {
+    const InfLayerDesc& d = desc->layers[i];
+    if (d.kind == INF_LAYER_CONV || d.kind == INF_LAYER_LINEAR) {
+      WLayer w;
+      w.kind = d.kind;
+      w.cin = d.cin;
+      w.cout = d.cout;
+      w.ks = d.kind == INF_LAYER_LINEAR ? 1 : d.ksize;
+      w.W = d.weight;
+      w.b = d.bias;
+      w.u = d.u;
+      w.v = d.v;
+      w.coeff = d.coeff;
+      if (w.ks != 1 && w.ks != 3) { delete n; return INF_ERR_UNSUPPORTED; }
+      if (!w.b) { delete n; return INF_ERR_UNSUPPORTED; }
+      n->L.push_back(w);
+    } else if (d.kind == INF_ACT_SWISH || d.kind == INF_ACT_SIN) {
+      if (n->L.empty() || n->L.back().act != ACT_NONE) { delete n; return INF_ERR_UNSUPPORTED; }
+      n->L.back().act = d.kind == INF_ACT_SWISH ? ACT_SWISH : ACT_SIN;
+      n->L.back().act_beta = d.beta;
+    } else {
+      delete n;
+      return INF_ERR_INVALID;
+    }
+  }
+  const int L = (int)n->L.size();
+  if (L == 0 || n->L.back().act != ACT_NONE) { delete n; return INF_ERR_UNSUPPORTED; }
+  n->fc = n->L[0].kind == INF_LAYER_LINEAR;
+  if (n->fc) {
+    n->d = n->C;
+    n->P = 1;
+  }
+  // channel chain: C -> ... -> C
+  int ch = n->C;
+  for (auto& w : n->L) {
+    if (w.cin != ch || (n->fc && w.kind != INF_LAYER_LINEAR) || (!n->fc && w.kind != INF_LAYER_CONV)) {
+      delete n;
+      return INF_ERR_UNSUPPORTED;
+    }
+    ch = w.cout;
+  }
+  if (ch != n->C) { delete n; return INF_ERR_UNSUPPORTED; }
+  if (n->fc && n->C > 32) { delete n; return INF_ERR_UNSUPPORTED; }
+  // plans
+  size_t floats = 0;
+  for (int l = 0; l < L; ++l) {
+    WLayer& w = n->L[l];
+    const bool last = l == L - 1, first = l == 0;
+    if (l < L - 1) n->hidden_max = std::max(n->hidden_max, w.cout);
+    // forward operand
+    if (w.ks == 1) {
+      w.f = Operand{BL_DIRECT, 0, w.cout, 0, w.cin, 0, PK_ROWMAJOR, nullptr};
+    } else if (last && w.cout < TAPS_MAX_CH) {
+      w.f = Operand{BL_DIRECT, 1, 9 * w.cout, 0, w.cin, 0, PK_TAPS_FWD, nullptr};
+    } else {
+      w.f = Operand{BL_IM2COL3, 0, w.cout, 0, 9 * w.cin, 0, PK_IM2COL_FWD, nullptr};
+    }
+    if (!last && w.f.taps) { delete n; return INF_ERR_UNSUPPORTED; }
+    // vjp operand (maps grad wrt output -> grad wrt input)
+    if (w.ks == 1) {
+      w.g = Operand{BL_DIRECT, 0, w.cin, 0, w.cout, 0, PK_TRANSPOSE, nullptr};
+    } else if (first && w.cin < TAPS_MAX_CH) {
+      w.g = Operand{BL_DIRECT, 1, 9 * w.cin, 0, w.cout, 0, PK_TAPS_BWD, nullptr};
+    } else {
+      w.g = Operand{BL_IM2COL3, 0, w.cin, 0, 9 * w.cout, 0, PK_IM2COL_BWD, nullptr};
+    }
+    for (Operand* op : {&w.f, &w.g}) {
+      op->Mpad = round_up(op->M, 128);
+      op->Kpad = round_up(op->K, 16);
+      floats += (size_t)op->Mpad * op->Kpad + 64;
+    }
+    floats += 64;   // factor
+    if (last) n->rows_max = std::max(n->rows_max, w.f.M);
+    if (first) n->rows_max = std::max(n->rows_max, w.g.M);
+  }
+  if (L == 1) n->hidden_max = std::max(n->hidden_max, 1);
+  // sigma scratch: one partial per 256 output elements of the largest conv
+  size_t sc = 64;
+  for (auto& w : n->L) sc = std::max(sc, (size_t)w.cout * (n->fc ? 1 : n->P) / 256 + 64);
+  n->scratch_doubles = sc;
+  if (hipGetDevice(&n->device) != hipSuccess) n->device = 0;
+  if (hipMalloc(&n->dev, floats * sizeof(float)) != hipSuccess ||
+      hipMalloc(&n->scratch, sc * sizeof(double)) != hipSuccess) {
+    if (n->dev) (void)hipFree(n->dev);
+    delete n;
+    return INF_ERR_HIP;
+  }
+  float* p = n->dev;
+  for (auto& w : n->L) {
+    for (Operand* op : {&w.f, &w.g}) {
+      op->A = p;
+      p += (size_t)op->Mpad * op->Kpad + 64;
+    }
+    w.factor = p;
+    p += 64;
+  }
+  *out = n;
+  return INF_OK;
+}
+
+int inf_net_destroy(InfNet* n) {
+  if (!n) return INF_OK;
+  if (n->dev) (void)hipFree(n->dev);
+  if (n->scratch) (void)hipFree(n->scratch);
+  delete n;
+  return INF_OK;
+}
+
+int inf_net_refresh(InfNet* n, void* stream) {
+  if (!n) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  for (auto& w : n->L) {
+    const int H = n->fc ? 1 : (w.ks == 1 ? 1 : n->H), Wd = n->fc ? 1 : (w.ks == 1 ? 1 : n->W);
+    INF_TRY(launch_sigma(w.W, w.u, w.v, w.cout, w.cin, w.ks, H, Wd, w.coeff, w.factor,
+                         reinterpret_cast<float*>(n->scratch), s));
+    INF_TRY(launch_pack(w.W, w.factor, w.f.A, w.cout, w.cin, w.ks, w.f.Mpad, w.f.Kpad, w.f.pack, s));
+    INF_TRY(launch_pack(w.W, w.factor, w.g.A, w.cout, w.cin, w.ks, w.g.Mpad, w.g.Kpad, w.g.pack, s));
+  }
+  return INF_OK;
+}
+
+size_t inf_workspace_bytes(const InfNet* n, int batch, int threshold) {
+  if (!n || batch <= 0) return 0;
+  return ws_need(n, batch, std::max(threshold, 1));
+}
+
+int inf_net_forward(InfNet* n, const float* x, float* y, int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !y || B <= 0) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.out0 = n->fc ? bf.tmp : y;
+  INF_TRY(run_forward(n, xi, B, bf, OM_PLAIN, &a, s));
+  if (n->fc) INF_TRY(to_boundary(n, bf.tmp, y, B, s));
+  return INF_OK;
+}
+
+int inf_net_vjp(InfNet* n, const float* x, const float* v, float* out, int B, void* ws, size_t ws_bytes,
+                void* stream) {
+  if (!n || !x || !v || !out || B <= 0) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* vi = to_internal(n, v, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(run_forward(n, xi, B, bf, -1, nullptr, s));
+  float* o = n->fc ? bf.tmp : out;
+  INF_TRY(run_vjp(n, vi, o, xi, nullptr, nullptr, B, bf, s));
+  if (n->fc) INF_TRY(to_boundary(n, bf.tmp, out, B, s));
+  return INF_OK;
+}
+
+static int root_find_common(InfNet* f, InfNet* e, const float* y, int B, int T, double eps, InfBroydenStats* stats,
+                            float* diff_detail, Bufs& bf, const float** yi_out, hipStream_t s) {
+  int st = INF_OK;
+  const float* yi = to_internal(f, y, bf.xin, B, s, &st);
+  INF_TRY(st);
+  // x_embed = e(y) + y ; fx = e(y)   (implicit_block.py:71)
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = yi;
+  a.out0 = bf.fx;
+  a.out1 = bf.xemb;
+  INF_TRY(run_forward(e, yi, B, bf, OM_EMBED, &a, s));
+  INF_TRY(broyden_solve(f, yi, B, T, eps, stats, diff_detail, bf, s));
+  *yi_out = yi;
+  return INF_OK;
+}
+
+int inf_root_find(InfNet* f, InfNet* e, const float* y, float* out, int B, int T, double eps, InfBroydenStats* stats,
+                  float* diff_detail, void* ws, size_t ws_bytes, void* stream) {
+  if (!f || !e || !y || !out || B <= 0 || T <= 0 || T > 64 || !same_shape(f, e)) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(f, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const float* yi;
+  INF_TRY(root_find_common(f, e, y, B, T, eps, stats, diff_detail, bf, &yi, s));
+  return to_boundary(f, bf.lowest, out, B, s);
+}
+
+int inf_imblock_forward(InfNet* nx, InfNet* nz, const float* x, float* z, int B, int T, double eps,
+                        InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
+  if (!nx || !nz || !x || !z || B <= 0 || T <= 0 || T > 64 || !same_shape(nx, nz)) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(nx, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const float* xi;
+  INF_TRY(root_find_common(nz, nx, x, B, T, eps, stats, nullptr, bf, &xi, s));
+  // z = (nnet_x(x) - nnet_z(z*)) + x   (implicit_block.py:227)
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = bf.fx;
+  a.in1 = xi;
+  a.out0 = nx->fc ? bf.tmp : z;
+  INF_TRY(run_forward(nz, bf.lowest, B, bf, OM_RECOMP, &a, s));
+  if (nx->fc) INF_TRY(to_boundary(nx, bf.tmp, z, B, s));
+  return INF_OK;
+}
+
+int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
+                      int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !vareps || !coeff || !out || B <= 0 || n_terms < 0 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  if (n_terms == 0) {
+    INF_HIP(hipMemsetAsync(out, 0, sizeof(float) * B, s));
+    return INF_OK;
+  }
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(run_forward(n, xi, B, bf, -1, nullptr, s));
+  const float* v = ei;
+  for (int k = 0; k < n_terms; ++k) {
+    float* vo = (k % 2 == 0) ? bf.va : bf.vb;
+    INF_TRY(run_vjp(n, v, vo, xi, ei, bf.part + (size_t)k * B * bf.nchunk, B, bf, s));
+    v = vo;
+  }
+  return launch_series_combine(bf.part, coeff, n_terms, B, bf.nchunk, out, s);
+}
+
+int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,
+                       int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !vareps || !ncoeff || !out || B <= 0 || n_terms < 0) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const size_t E = (size_t)B * n->d;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(run_forward(n, xi, B, bf, -1, nullptr, s));
+  // neumann_vjp = vareps ; vjp = vareps
+  INF_HIP(hipMemcpyAsync(bf.tmp, ei, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  const float* v = ei;
+  for (int k = 1; k <= n_terms; ++k) {
+    float* vo = (k % 2 == 1) ? bf.va : bf.vb;
+    INF_TRY(run_vjp(n, v, vo, xi, nullptr, nullptr, B, bf, s));
+    INF_TRY(glue_axpy_scaled(bf.tmp, vo, ncoeff[k], (long)E, s));
+    v = vo;
+  }
+  INF_TRY(run_vjp(n, bf.tmp, bf.va, xi, ei, bf.part, B, bf, s));
+  const float one = 1.f;
+  return launch_series_combine(bf.part, &one, 1, B, bf.nchunk, out, s);
+}
+
+int inf_logdet_exact(InfNet* n, const float* x, float* out, int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !out || B <= 0) return INF_ERR_INVALID;
+  if (!n->fc || n->d > 16 || n->pre_act != ACT_NONE) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const int d = n->d;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(glue_init_tangents(xi, bf.ext0, d, B, s));
+  const int cols = (d + 1) * B;
+  const float* cur = bf.ext0;
+  for (size_t l = 0; l < n->L.size(); ++l) {
+    const WLayer& w = n->L[l];
+    float* o = (l % 2 == 0) ? bf.ext1 : bf.ext0;
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = w.f.A;
+    g.M = w.f.M;
+    g.Kpad = w.f.Kpad;
+    g.Ktot = w.f.K;
+    g.X = cur;
+    g.x_sample = 0;
+    g.P = cols;
+    g.N = cols;
+    g.H = 1;
+    g.W = cols;
+    g.out = o;
+    g.o_sample = 0;
+    g.bias = w.b;
+    g.n_primal = B;
+    INF_TRY(launch_gemm(g, BL_DIRECT, EP_BIAS_PRIMAL, s));
+    if (w.act != ACT_NONE) INF_TRY(launch_fwdmode_act(o, nullptr, w.cout, B, d, w.act, w.act_beta, s));
+    cur = o;
+  }
+  return launch_logdet_small(cur, out, d, B, B, s);
+}
+
+size_t inf_broyden_workspace_bytes(int batch, int d, int threshold) {
+  const size_t nchunk = (size_t)(d + 1023) / 1024;
+  return sizeof(double) * ((size_t)batch * nchunk * (3 * (size_t)threshold + 2) + 64);
+}
+
+int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, const float* gx, const float* x,
+                       float* update, float* x_next, float* dx_next, int B, int d, int T, int nstep, void* ws,
+                       size_t ws_bytes, void* stream) {
+  if (!U || !VT || !dx || !dg || !gx || !x || !update || !x_next || !dx_next || B <= 0 || d <= 0 || T <= 0 ||
+      T > 64 || nstep < 1 || nstep > T)
+    return INF_ERR_INVALID;
+  if (!ws || ws_bytes < inf_broyden_workspace_bytes(B, d, T)) return INF_ERR_WORKSPACE;
+  BroydenArgs ba;
+  memset(&ba, 0, sizeof(ba));
+  ba.batch = B;
+  ba.d = d;
+  ba.T = T;
+  ba.sb = d;
+  ba.si = 1;
+  ba.cs = (long)B * d;
+  ba.U = U;
+  ba.VT = VT;
+  ba.dx = dx;
+  ba.dg = dg;
+  ba.gx = gx;
+  ba.x = x;
+  ba.xnew = x_next;
+  ba.dxnew = dx_next;
+  ba.upd = update;
+  ba.part = reinterpret_cast<double*>(ws);
+  ba.m = (nstep - 1) % T;
+  ba.ncols = std::min(nstep, T);
+  return launch_broyden_update(ba, (hipStream_t)stream);
+}
+
+// ---- flow glue ------------------------------------------------------------------------------
+int inf_logit_forward(const float* x, float* y, const float* logp_in, float* logp_out, int B, int per, float alpha,
+                      void* stream) {
+  if (!x || !y || !logp_out || B <= 0 || per <= 0) return INF_ERR_INVALID;
+  return glue_logit(x, y, logp_in, logp_out, B, per, alpha, (hipStream_t)stream);
+}
+int inf_actnorm_forward(const float* x, float* y, const float* w, const float* b, const float* logp_in,
+                        float* logp_out, int B, int C, int hw, void* stream) {
+  if (!x || !y || !w || !b || B <= 0) return INF_ERR_INVALID;
+  return glue_actnorm(x, y, w, b, logp_in, logp_out, B, C, hw, (hipStream_t)stream);
+}
+int inf_squeeze2(const float* x, float* y, int B, int C, int H, int W, void* stream) {
+  if (!x || !y || B <= 0 || (H & 1) || (W & 1)) return INF_ERR_INVALID;
+  return glue_squeeze2(x, y, B, C, H, W, (hipStream_t)stream);
+}
+int inf_normal_logprob(const float* z, float* out, int B, int per, void* stream) {
+  if (!z || !out || B <= 0) return INF_ERR_INVALID;
+  return glue_normal_logprob(z, out, B, per, (hipStream_t)stream);
+}
+int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* stream) {
+  if (!out && n) return INF_ERR_INVALID;
+  return glue_rademacher(out, n, seed, offset, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+// Flow glue around the imBlocks (K9 of SURVEY.md §2.3) and small solver helpers.
+//   LogitTransform (elemwise.py:112-128), ActNorm (act_norm.py:153-193), squeeze (squeeze.py:242-255),
+//   standard normal log-prob (train_img.py:135-137), Rademacher probes, Banach fixed-point test
+//   (implicit_block.py:17-28), Neumann accumulation (implicit_block.py:435), forward-mode tangents.
+#include "kernels.h"
+#include "glue.h"
+
+namespace inf {
+
+// one block per sample: y = logit(alpha + (1-2a)x);  logp_out = logp_in - sum(-log(s - s*s) + log(1-2a))
+__global__ __launch_bounds__(256) void logit_kernel(const float* x, float* y, const float* lin, float* lout, int per,
+                                                    float alpha) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const float* xb = x + (long)b * per;
+  float* yb = y + (long)b * per;
+  const float c1 = 1.f - 2.f * alpha;
+  const float lc = logf(c1);
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < per; i += blockDim.x) {
+    const float s = alpha + c1 * xb[i];
+    yb[i] = logf(s) - logf(1.f - s);
+    acc += (double)(-logf(s - s * s) + lc);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) lout[b] = (lin ? lin[b] : 0.f) - (float)acc;
+}
+
+// one block per sample: y = (x + b_c) * exp(w_c); logp_out = logp_in - hw * sum_c w_c
+__global__ __launch_bounds__(256) void actnorm_kernel(const float* x, float* y, const float* w, const float* bias,
+                                                      const float* lin, float* lout, int C, int hw) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const long per = (long)C * hw;
+  const float* xb = x + b * per;
+  float* yb = y + b * per;
+  for (long i = threadIdx.x; i < per; i += blockDim.x) {
+    const int c = i / hw;
+    yb[i] = (xb[i] + bias[c]) * expf(w[c]);
+  }
+  double acc = 0.0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) acc += (double)w[c] * hw;
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0 && lout) lout[b] = (lin ? lin[b] : 0.f) - (float)acc;
+}
+
+// (B,C,H,W) -> (B,4C,H/2,W/2): out[b][c*4 + ry*2 + rx][y][x] = in[b][c][2y+ry][2x+rx]
+__global__ void squeeze2_kernel(const float* x, float* y, int C, int H, int W, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int Ho = H / 2, Wo = W / 2;
+  long t = i;
+  const int xo = t % Wo; t /= Wo;
+  const int yo = t % Ho; t /= Ho;
+  const int co = t % (4 * C); t /= (4 * C);
+  const long b = t;
+  const int c = co >> 2, ry = (co >> 1) & 1, rx = co & 1;
+  y[i] = x[((b * C + c) * H + 2 * yo + ry) * W + 2 * xo + rx];
+}
+
+__global__ __launch_bounds__(256) void normal_logprob_kernel(const float* z, float* out, int per) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const float* zb = z + (long)b * per;
+  const float logZ = -0.5f * logf(2.f * 3.14159265358979323846f);
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < per; i += blockDim.x) {
+    const float v = zb[i];
+    acc += (double)(logZ - v * v / 2.f);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[b] = (float)acc;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__global__ void rademacher_kernel(float* out, size_t n, uint64_t seed, uint64_t offset) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(seed * 0x2545F4914F6CDD1DULL + offset + i);
+  out[i] = (h >> 63) ? 1.f : -1.f;
+}
+
+// Banach iteration test (implicit_block.py:21): count elements with (x - xp)^2 / (eps + eps*|y|) >= 1
+__global__ void fixed_point_check_kernel(const float* x, const float* xp, const float* y, long n, float eps,
+                                         unsigned int* count) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (i < n) {
+    const float d = x[i] - xp[i];
+    const float tol = eps + eps * fabsf(y[i]);
+    bad = !((d * d) / tol < 1.f);
+  }
+  const unsigned long long m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned int)__popcll(m));
+}
+
+// y = y + c * x   (neumann_vjp + (-1)**k * coeff_fn(k) * vjp)
+__global__ void axpy_scaled_kernel(float* y, const float* x, float c, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = y[i] + c * x[i];
+}
+
+// ext (d, (1+d)B): primal block = x (d, B) feature-major, tangent block j = unit vector e_{j-1}
+__global__ void init_tangents_kernel(const float* xT, float* ext, int d, int B) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long ld = (long)(d + 1) * B;
+  if (i >= (long)d * ld) return;
+  const int f = i / ld;
+  const long col = i - (long)f * ld;
+  const int j = col / B, b = col - (long)j * B;
+  ext[i] = j == 0 ? xT[(long)f * B + b] : (f == j - 1 ? 1.f : 0.f);
+}
+
+#define GRID1(n) dim3((unsigned)(((n) + 255) / 256)), dim3(256)
+
+int glue_logit(const float* x, float* y, const float* lin, float* lout, int B, int per, float alpha, hipStream_t s) {
+  hipLaunchKernelGGL(logit_kernel, dim3(B), dim3(256), 0, s, x, y, lin, lout, per, alpha);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_actnorm(const float* x, float* y, const float* w, const float* b, const float* lin, float* lout, int B, int C,
+                 int hw, hipStream_t s) {
+  hipLaunchKernelGGL(actnorm_kernel, dim3(B), dim3(256), 0, s, x, y, w, b, lin, lout, C, hw);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_squeeze2(const float* x, float* y, int B, int C, int H, int W, hipStream_t s) {
+  const long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(squeeze2_kernel, GRID1(n), 0, s, x, y, C, H, W, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_normal_logprob(const float* z, float* out, int B, int per, hipStream_t s) {
+  hipLaunchKernelGGL(normal_logprob_kernel, dim3(B), dim3(256), 0, s, z, out, per);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, hipStream_t s) {
+  if (n == 0) return INF_OK;
+  hipLaunchKernelGGL(rademacher_kernel, GRID1(n), 0, s, out, n, seed, offset);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_fixed_point_check(const float* x, const float* xp, const float* y, long n, float eps, unsigned int* count,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(fixed_point_check_kernel, GRID1(n), 0, s, x, xp, y, n, eps, count);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_axpy_scaled(float* y, const float* x, float c, long n, hipStream_t s) {
+  hipLaunchKernelGGL(axpy_scaled_kernel, GRID1(n), 0, s, y, x, c, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int glue_init_tangents(const float* xT, float* ext, int d, int B, hipStream_t s) {
+  const long n = (long)d * (d + 1) * B;
+  hipLaunchKernelGGL(init_tangents_kernel, GRID1(n), 0, s, xT, ext, d, B);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+}  // namespace inf

@@ -1,0 +1,112 @@
+// Internal kernel launch interfaces (host side) for libinflow.
+#pragma once
+#include "common.h"
+
+namespace inf {
+
+// ------------------------------------------------------------------------------------------
+// GEMM:  out[b][m][p] = epi( sum_k A[m][k] * Bop[k][n] ),  n = b * P + p
+//   A: (Mpad, Kpad) row-major, zero padded (Mpad multiple of 128, Kpad multiple of 16)
+//   Bop from X by one of the loaders below.  f32 in / f32 accumulate (v_mfma_f32_32x32x2_f32).
+// ------------------------------------------------------------------------------------------
+enum BLoad { BL_DIRECT = 0, BL_IM2COL3 = 1 };
+enum Epi { EP_STORE = 0, EP_BIAS = 1, EP_BIAS_ACT = 2, EP_MUL_DERIV = 3, EP_BIAS_PRIMAL = 4,
+           // compile-time activation variants of EP_BIAS_ACT (selected by launch_gemm from GemmArgs::act)
+           EP_ACT_SWISH = 5, EP_ACT_SIN = 6, EP_ACT_NONE = 7 };
+
+struct GemmArgs {
+  const float* A;
+  int M, Kpad, Ktot;
+  const float* X;         // B-operand source (NCHW; DIRECT: (B, K, P); IM2COL3: (B, Cin, H, W))
+  long x_sample;          // sample stride of X in elements
+  int P;                  // pixels (columns) per sample
+  int N;                  // total columns
+  int H, W;               // IM2COL3 geometry (P = H * W)
+  const float* pre_beta;  // loader applies swish(., softplus(*pre_beta)) to X when non-null
+  float* out;
+  long o_sample;          // output sample stride (channel stride is P)
+  const float* bias;
+  int act;                // Act for EP_BIAS_ACT
+  const float* act_beta;  // swish beta
+  float* deriv_out;       // EP_BIAS_ACT: act'(a) saved here when non-null
+  int write_out;          // EP_BIAS_ACT: write act(a)
+  const float* deriv_in;  // EP_MUL_DERIV multiplier (same indexing as out)
+  int n_primal;           // EP_BIAS_PRIMAL: columns n < n_primal get the bias
+};
+int launch_gemm(const GemmArgs& g, int bload, int epi, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// Output stage of a conv net whose last layer produced packed taps Y[b][c*9+t][p] (ks = 3) or
+// plain rows Y[b][c][p] (ks = 1): s = sum_t Y[..][shift_t(p)], then a fused epilogue.
+// ------------------------------------------------------------------------------------------
+enum OutMode { OM_PLAIN = 0, OM_EMBED = 1, OM_RESID = 2, OM_RECOMP = 3, OM_VJP = 4 };
+struct OutArgs {
+  const float* Y;
+  long y_sample;
+  int C, H, W, ks;
+  int mode;
+  const float* bias;
+  const float* in0;
+  const float* in1;
+  const float* in2;
+  float* out0;
+  float* out1;
+  const float* pre_beta;  // OM_VJP: multiply by swish'(in1) (preact input derivative)
+  double* partial;        // (B, nchunk) per-sample partial sums (OM_RESID: g^2, OM_VJP: v.eps)
+  int nchunk;
+};
+int out_nchunk(int per_sample);
+int launch_conv_out(const OutArgs& a, int batch, hipStream_t s);
+
+// fc nets: feature-major (d, B) tensors, one thread per sample for the per-sample reductions.
+int launch_fc_out(const OutArgs& a, int batch, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// misc elementwise / layout
+// ------------------------------------------------------------------------------------------
+int launch_transpose(const float* x, float* y, int rows, int cols, hipStream_t s);  // y[c][r] = x[r][c]
+int launch_axpy_step(const float* x, const float* upd, float* xnew, float* dx, long n, hipStream_t s);
+int launch_neg(const float* x, float* y, long n, hipStream_t s);
+int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// Broyden low-rank algebra (broyden.py:101-120,174-181), per-sample, layout-generic:
+//   element i of sample b lives at b * sb + i * si;  U/VT column j of sample b at
+//   j * cs + b * sb + i * si  (cs = column stride).
+// ------------------------------------------------------------------------------------------
+struct BroydenArgs {
+  int batch, d, T;
+  long sb, si, cs;
+  float* U;
+  float* VT;
+  const float* dx;
+  const float* dg;
+  const float* gx;
+  const float* x;
+  float* xnew;
+  float* dxnew;
+  float* upd;
+  double* part;   // scratch partials
+  int m;          // existing columns (nstep - 1) % T
+  int ncols;      // columns used by the update (min(nstep, T))
+};
+int launch_broyden_update(const BroydenArgs& a, hipStream_t s);
+
+// Spectral scale: sigma = u . (W v) for conv (pad k//2) or matrix; factor = max(1, sigma / coeff)
+int launch_sigma(const float* W, const float* u, const float* v, int cout, int cin, int ks, int H, int Wd,
+                 float coeff, float* factor_out, float* scratch, hipStream_t s);
+// Packed operand:  dst[(mrow)][kcol] built from W / factor with the given pack mode.
+enum PackMode { PK_ROWMAJOR = 0, PK_TRANSPOSE = 1, PK_IM2COL_FWD = 2, PK_IM2COL_BWD = 3, PK_TAPS_FWD = 4,
+                PK_TAPS_BWD = 5 };
+int launch_pack(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad, int Kpad,
+                int mode, hipStream_t s);
+
+// exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
+int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
+int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, int act, const float* beta,
+                       hipStream_t s);
+
+int launch_series_combine(const double* partials, const float* coeff_dev, int n_terms, int batch, int nchunk,
+                          float* out, hipStream_t s);
+
+}  // namespace inf

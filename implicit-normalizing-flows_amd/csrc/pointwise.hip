@@ -1,0 +1,582 @@
+// HBM-bound kernels of the hot path: the conv-net output stage (tap sum + fused residual / trace
+// epilogues), Broyden low-rank algebra, spectral normalisation + operand packing, exact small
+// log-dets, and layout helpers.  All are coalesced over the contiguous per-sample dimension and
+// reduce per sample with wave shuffles + one LDS stage; cross-block sums go through fixed-order
+// fp64 partial slabs (deterministic, no float atomics).
+#include "kernels.h"
+
+namespace inf {
+
+constexpr int OUT_CH = 1024;   // elements per block in conv_out (256 threads x 4)
+
+int out_nchunk(int per_sample) { return (per_sample + OUT_CH - 1) / OUT_CH; }
+
+// ------------------------------------------------------------------------------------------
+// conv net output stage.  Y holds packed taps Y[b][c*9+t][p] (KS = 3) or rows Y[b][c][p] (KS = 1).
+//   s = sum_t Y[b][c*9+t][p + (dy-1, dx-1)]           (zero padding outside the image)
+// then (implicit_block.py:60,72,227,422-423):
+//   OM_PLAIN : out0 = s + bias
+//   OM_EMBED : out0 = a = s + bias (= nnet_x(x));  out1 = a + x   (x_embed)
+//   OM_RESID : out0 = g = (x_embed - a) - z;  out1 = g - g_prev;  partial += g^2
+//   OM_RECOMP: out0 = (fx - a) + x
+//   OM_VJP   : out0 = v = s (* swish'(x_in) for preact nets);  partial += v * eps
+// ------------------------------------------------------------------------------------------
+template <int KS>
+__global__ __launch_bounds__(256) void conv_out_kernel(OutArgs a) {
+  __shared__ double red[16];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int P = a.H * a.W, per = a.C * P;
+  const long ybase = (long)b * a.y_sample, ebase = (long)b * per;
+  const float sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+  const int lo = chunk * OUT_CH, hi = min(per, lo + OUT_CH);
+  double acc = 0.0;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int c = i / P, p = i - c * P;
+    float s;
+    if constexpr (KS == 1) {
+      s = a.Y[ybase + (long)c * P + p];
+    } else {
+      const int y = p / a.W, x = p - y * a.W;
+      const float* yc = a.Y + ybase + (long)c * 9 * P;
+      s = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) s += yc[(long)t * P + yy * a.W + xx];
+      }
+    }
+    const long ei = ebase + i;
+    switch (a.mode) {
+      case OM_PLAIN: a.out0[ei] = s + a.bias[c]; break;
+      case OM_EMBED: {
+        const float v = s + a.bias[c];
+        a.out0[ei] = v;
+        a.out1[ei] = v + a.in0[ei];
+        break;
+      }
+      case OM_RESID: {
+        const float v = s + a.bias[c];
+        const float gx = (a.in0[ei] - v) - a.in1[ei];
+        a.out0[ei] = gx;
+        if (a.in2) a.out1[ei] = gx - a.in2[ei];
+        acc += (double)gx * (double)gx;
+        break;
+      }
+      case OM_RECOMP: a.out0[ei] = (a.in0[ei] - (s + a.bias[c])) + a.in1[ei]; break;
+      default: {  // OM_VJP
+        float v = s;
+        if (a.pre_beta) v = v * swish_d(a.in1[ei], sp);
+        a.out0[ei] = v;
+        if (a.partial) acc += (double)v * (double)a.in0[ei];
+      }
+    }
+  }
+  if (a.partial) {
+    const double t = block_sum(acc, red);
+    if (threadIdx.x == 0) a.partial[(long)b * a.nchunk + chunk] = t;
+  }
+}
+
+int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
+  const int per = a.C * a.H * a.W;
+  dim3 grid(out_nchunk(per), batch);
+  if (a.ks == 1)
+    hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv_out_kernel<3>, grid, dim3(256), 0, s, a);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// fc nets: tensors are feature-major (d, B); Y rows are (d, B); one thread per sample.
+__global__ __launch_bounds__(256) void fc_out_kernel(OutArgs a, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const float sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+  double acc = 0.0;
+  for (int c = 0; c < a.C; ++c) {
+    const long ei = (long)c * batch + b;
+    const float s = a.Y[ei];
+    switch (a.mode) {
+      case OM_PLAIN: a.out0[ei] = s + a.bias[c]; break;
+      case OM_EMBED: {
+        const float v = s + a.bias[c];
+        a.out0[ei] = v;
+        a.out1[ei] = v + a.in0[ei];
+        break;
+      }
+      case OM_RESID: {
+        const float v = s + a.bias[c];
+        const float gx = (a.in0[ei] - v) - a.in1[ei];
+        a.out0[ei] = gx;
+        if (a.in2) a.out1[ei] = gx - a.in2[ei];
+        acc += (double)gx * (double)gx;
+        break;
+      }
+      case OM_RECOMP: a.out0[ei] = (a.in0[ei] - (s + a.bias[c])) + a.in1[ei]; break;
+      default: {
+        float v = s;
+        if (a.pre_beta) v = v * swish_d(a.in1[ei], sp);
+        a.out0[ei] = v;
+        if (a.partial) acc += (double)v * (double)a.in0[ei];
+      }
+    }
+  }
+  if (a.partial) a.partial[b] = acc;
+}
+
+int launch_fc_out(const OutArgs& a, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(fc_out_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, a, batch);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// layout / small vector helpers
+// ------------------------------------------------------------------------------------------
+__global__ void transpose_kernel(const float* x, float* y, int rows, int cols) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const int r = i / cols, c = i - (long)r * cols;
+  y[(long)c * rows + r] = x[i];
+}
+int launch_transpose(const float* x, float* y, int rows, int cols, hipStream_t s) {
+  const long n = (long)rows * cols;
+  if (n == 0) return INF_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, y, rows, cols);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// x_est = x0 + update; delta_x = x_est - x0   (line_search(on=False): broyden.py:94-99)
+__global__ void axpy_step_kernel(const float* x, const float* upd, float* xnew, float* dx, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x0 = x[i];
+  const float xe = x0 + upd[i];
+  xnew[i] = xe;
+  dx[i] = xe - x0;
+}
+int launch_axpy_step(const float* x, const float* upd, float* xnew, float* dx, long n, hipStream_t s) {
+  hipLaunchKernelGGL(axpy_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, xnew, dx, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+__global__ void neg_kernel(const float* x, float* y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = -x[i];
+}
+int launch_neg(const float* x, float* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(neg_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, y, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+__global__ void reduce_partials_kernel(const double* partial, int batch, int nchunk, double* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunk; ++c) s += partial[(long)b * nchunk + c];
+  out[b] = s;
+}
+int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, partial, batch, nchunk,
+                     out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Broyden low-rank update (broyden.py:174-181) with H = -I + U V^T:
+//   a_j = dx.U_j, c_j = VT_j.dg      (j < m)
+//   vT  = -dx + sum_j a_j VT_j                  (rmatvec, :101-109)
+//   u   = (dx - (-dg + sum_j c_j U_j)) / (vT.dg)   (matvec, :112-120)
+//   NaN -> 0 in vT and u; store column m
+//   e_j = VT_j.gx (j < ncols);  update = -(-gx + sum_j e_j U_j);  x_new = x + update
+// ------------------------------------------------------------------------------------------
+constexpr int BR_CH = 1024;   // elements per block (256 threads x 4)
+constexpr int BR_TMAX = 64;
+
+#define BR_IDX(b, i) ((long)(b) * a.sb + (long)(i) * a.si)
+
+// one thread per sample (small d: fc nets)
+__global__ __launch_bounds__(256) void broyden_small_kernel(BroydenArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.batch) return;
+  float aj[BR_TMAX], cj[BR_TMAX];
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    double sa = 0.0, sc = 0.0;
+    for (int i = 0; i < a.d; ++i) {
+      const long e = BR_IDX(b, i);
+      sa += (double)a.dx[e] * U[e];
+      sc += (double)V[e] * a.dg[e];
+    }
+    aj[j] = (float)sa;
+    cj[j] = (float)sc;
+  }
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  double den = 0.0;
+  for (int i = 0; i < a.d; ++i) {
+    const long e = BR_IDX(b, i);
+    float vt = -a.dx[e], t = -a.dg[e];
+    for (int j = 0; j < a.m; ++j) {
+      vt += aj[j] * a.VT[(long)j * a.cs + e];
+      t += cj[j] * a.U[(long)j * a.cs + e];
+    }
+    Vm[e] = vt;
+    Um[e] = a.dx[e] - t;
+    den += (double)vt * a.dg[e];
+  }
+  const float denf = (float)den;
+  for (int i = 0; i < a.d; ++i) {
+    const long e = BR_IDX(b, i);
+    float vt = Vm[e];
+    float u = Um[e] / denf;
+    if (vt != vt) vt = 0.f;
+    if (u != u) u = 0.f;
+    Vm[e] = vt;
+    Um[e] = u;
+  }
+  float ej[BR_TMAX];
+  for (int j = 0; j < a.ncols; ++j) {
+    const float* V = a.VT + (long)j * a.cs;
+    double se = 0.0;
+    for (int i = 0; i < a.d; ++i) se += (double)V[BR_IDX(b, i)] * a.gx[BR_IDX(b, i)];
+    ej[j] = (float)se;
+  }
+  for (int i = 0; i < a.d; ++i) {
+    const long e = BR_IDX(b, i);
+    float t = -a.gx[e];
+    for (int j = 0; j < a.ncols; ++j) t += ej[j] * a.U[(long)j * a.cs + e];
+    const float up = -t;
+    a.upd[e] = up;
+    const float x0 = a.x[e];
+    const float xe = x0 + up;
+    a.xnew[e] = xe;
+    a.dxnew[e] = xe - x0;
+  }
+}
+
+// chunked multi-kernel version (large d: conv nets), grid (nchunk, B), 256 threads
+// part layout: [B][nchunk][2*T] for phase 1, [B][nchunk] (+ offset) for phase 2, [B][nchunk][T] for phase 3
+__global__ __launch_bounds__(256) void broyden_p1(BroydenArgs a, int nchunk) {
+  __shared__ double red[16];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
+  double* out = a.part + ((long)b * nchunk + ch) * 2 * a.T;
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    double sa = 0.0, sc = 0.0;
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const long e = BR_IDX(b, i);
+      sa += (double)a.dx[e] * U[e];
+      sc += (double)V[e] * a.dg[e];
+    }
+    sa = block_sum(sa, red);
+    sc = block_sum(sc, red);
+    if (threadIdx.x == 0) {
+      out[j] = sa;
+      out[a.T + j] = sc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, double* part2) {
+  __shared__ double red[16];
+  __shared__ float coef[2 * BR_TMAX];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  for (int j = threadIdx.x; j < 2 * a.m; j += blockDim.x) {
+    const int jj = j < a.m ? j : a.T + (j - a.m);
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += a.part[((long)b * nchunk + c) * 2 * a.T + jj];
+    coef[j] = (float)s;   // a_j (j < m) then c_j
+  }
+  __syncthreads();
+  const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  double den = 0.0;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const long e = BR_IDX(b, i);
+    float vt = -a.dx[e], t = -a.dg[e];
+    for (int j = 0; j < a.m; ++j) {
+      vt += coef[j] * a.VT[(long)j * a.cs + e];
+      t += coef[a.m + j] * a.U[(long)j * a.cs + e];
+    }
+    Vm[e] = vt;
+    Um[e] = a.dx[e] - t;
+    den += (double)vt * a.dg[e];
+  }
+  den = block_sum(den, red);
+  if (threadIdx.x == 0) part2[(long)b * nchunk + ch] = den;
+}
+
+__global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, const double* part2, double* part3) {
+  __shared__ double red[16];
+  __shared__ float denf;
+  const int b = blockIdx.y, ch = blockIdx.x;
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += part2[(long)b * nchunk + c];
+    denf = (float)s;
+  }
+  __syncthreads();
+  const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const long e = BR_IDX(b, i);
+    float vt = Vm[e];
+    float u = Um[e] / denf;
+    if (vt != vt) vt = 0.f;
+    if (u != u) u = 0.f;
+    Vm[e] = vt;
+    Um[e] = u;
+  }
+  __syncthreads();
+  double* out = part3 + ((long)b * nchunk + ch) * a.T;
+  for (int j = 0; j < a.ncols; ++j) {
+    const float* V = a.VT + (long)j * a.cs;
+    double se = 0.0;
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const long e = BR_IDX(b, i);
+      se += (double)V[e] * a.gx[e];
+    }
+    se = block_sum(se, red);
+    if (threadIdx.x == 0) out[j] = se;
+  }
+}
+
+__global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, const double* part3) {
+  __shared__ float ej[BR_TMAX];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  for (int j = threadIdx.x; j < a.ncols; j += blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += part3[((long)b * nchunk + c) * a.T + j];
+    ej[j] = (float)s;
+  }
+  __syncthreads();
+  const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const long e = BR_IDX(b, i);
+    float t = -a.gx[e];
+    for (int j = 0; j < a.ncols; ++j) t += ej[j] * a.U[(long)j * a.cs + e];
+    const float up = -t;
+    a.upd[e] = up;
+    const float x0 = a.x[e];
+    const float xe = x0 + up;
+    a.xnew[e] = xe;
+    a.dxnew[e] = xe - x0;
+  }
+}
+
+int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
+  if (a.T > BR_TMAX || a.m >= a.T || a.ncols > a.T) return INF_ERR_INVALID;
+  if (a.d <= 32) {
+    hipLaunchKernelGGL(broyden_small_kernel, dim3((a.batch + 255) / 256), dim3(256), 0, s, a);
+    INF_CHECK_LAUNCH();
+    return INF_OK;
+  }
+  const int nchunk = (a.d + BR_CH - 1) / BR_CH;
+  dim3 grid(nchunk, a.batch);
+  double* part2 = a.part + (long)a.batch * nchunk * 2 * a.T;
+  double* part3 = part2 + (long)a.batch * nchunk;
+  if (a.m > 0) {
+    hipLaunchKernelGGL(broyden_p1, grid, dim3(256), 0, s, a, nchunk);
+    INF_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(broyden_p2, grid, dim3(256), 0, s, a, nchunk, part2);
+  INF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, part2, part3);
+  INF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, part3);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// spectral normalisation (mixed_lipschitz.py:126-132, 320-326, 378-386) and operand packing
+// ------------------------------------------------------------------------------------------
+// sigma partials: one thread per output element (o, y, x): (W v)[o,y,x] * u[o,y,x]
+__global__ __launch_bounds__(256) void sigma_partial_kernel(const float* W, const float* u, const float* v, int cout,
+                                                            int cin, int ks, int H, int Wd, double* part) {
+  __shared__ double red[16];
+  const int P = H * Wd;
+  const long n = (long)cout * P;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  double val = 0.0;
+  if (i < n) {
+    const int o = i / P, p = i - (long)o * P;
+    const int y = p / Wd, x = p - y * Wd;
+    const int pad = ks / 2;
+    float s = 0.f;
+    for (int c = 0; c < cin; ++c)
+      for (int dy = 0; dy < ks; ++dy)
+        for (int dx = 0; dx < ks; ++dx) {
+          const int yy = y + dy - pad, xx = x + dx - pad;
+          if (yy >= 0 && yy < H && xx >= 0 && xx < Wd)
+            s += W[(((long)o * cin + c) * ks + dy) * ks + dx] * v[((long)c * H + yy) * Wd + xx];
+        }
+    val = (double)s * (double)u[i];
+  }
+  val = block_sum(val, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = val;
+}
+__global__ void sigma_final_kernel(const double* part, int nparts, float coeff, float* factor) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nparts; ++i) s += part[i];
+  const float sigma = (float)s;
+  const float r = sigma / coeff;
+  factor[0] = r > 1.f ? r : 1.f;    // torch.max(ones(1), sigma / coeff)
+  factor[1] = sigma;
+}
+int launch_sigma(const float* W, const float* u, const float* v, int cout, int cin, int ks, int H, int Wd,
+                 float coeff, float* factor_out, float* scratch, hipStream_t s) {
+  const long n = (long)cout * H * Wd;
+  const int nb = (int)((n + 255) / 256);
+  double* part = reinterpret_cast<double*>(scratch);
+  hipLaunchKernelGGL(sigma_partial_kernel, dim3(nb), dim3(256), 0, s, W, u, v, cout, cin, ks, H, Wd, part);
+  INF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sigma_final_kernel, dim3(1), dim3(64), 0, s, part, nb, coeff, factor_out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+__global__ void pack_kernel(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad,
+                            int Kpad, int mode) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Mpad * Kpad) return;
+  const int m = i / Kpad, k = i - (long)m * Kpad;
+  const float f = factor[0];
+  const int kk = ks * ks;
+  int co = -1, ci = -1, t = 0;
+  switch (mode) {
+    case PK_ROWMAJOR: if (m < cout && k < cin) { co = m; ci = k; } break;
+    case PK_TRANSPOSE: if (m < cin && k < cout) { co = k; ci = m; } break;
+    case PK_IM2COL_FWD: if (m < cout && k < cin * kk) { co = m; ci = k / kk; t = k % kk; } break;
+    case PK_IM2COL_BWD: if (m < cin && k < cout * kk) { ci = m; co = k / kk; t = kk - 1 - k % kk; } break;
+    case PK_TAPS_FWD: if (m < cout * kk && k < cin) { co = m / kk; t = m % kk; ci = k; } break;
+    case PK_TAPS_BWD: if (m < cin * kk && k < cout) { ci = m / kk; t = kk - 1 - m % kk; co = k; } break;
+  }
+  dst[i] = co >= 0 ? W[((long)co * cin + ci) * kk + t] / f : 0.f;
+}
+int launch_pack(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad, int Kpad,
+                int mode, hipStream_t s) {
+  const long n = (long)Mpad * Kpad;
+  hipLaunchKernelGGL(pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, factor, dst, cout, cin, ks, Mpad, Kpad,
+                     mode);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// exact log|det(I + T)| per sample (torch.logdet via LU, implicit_block.py:253-258).  T is stored
+// feature-major as tangents: T[i][j] of sample b at tang[i * ld + (j + 1) * stride_j + b],
+// ld = (d + 1) * stride_j.  det <= 0 follows torch.logdet: NaN for negative, -inf for zero.
+// ------------------------------------------------------------------------------------------
+__global__ void logdet_small_kernel(const float* tang, float* out, int d, int batch, long stride_j) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  float M[16][16];
+  const long ld = (long)(d + 1) * stride_j;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) M[i][j] = (i == j ? 1.f : 0.f) + tang[i * ld + (j + 1) * stride_j + b];
+  float logabs = 0.f;
+  int sign = 1;
+  for (int k = 0; k < d; ++k) {
+    int piv = k;
+    float best = fabsf(M[k][k]);
+    for (int i = k + 1; i < d; ++i)
+      if (fabsf(M[i][k]) > best) { best = fabsf(M[i][k]); piv = i; }
+    if (piv != k) {
+      for (int j = 0; j < d; ++j) { const float t = M[k][j]; M[k][j] = M[piv][j]; M[piv][j] = t; }
+      sign = -sign;
+    }
+    const float pv = M[k][k];
+    if (pv == 0.f) { logabs = -INFINITY; sign = 0; break; }
+    if (pv < 0.f) sign = -sign;
+    logabs += logf(fabsf(pv));
+    for (int i = k + 1; i < d; ++i) {
+      const float f = M[i][k] / pv;
+      for (int j = k + 1; j < d; ++j) M[i][j] -= f * M[k][j];
+    }
+  }
+  out[b] = sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
+}
+int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s) {
+  if (d > 16) return INF_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(logdet_small_kernel, dim3((batch + 127) / 128), dim3(128), 0, s, tang, out, d, batch, stride_j);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// forward-mode activation on [primal | ntang tangent blocks], feature-major (d_out, (1+ntang)*B):
+// primal a -> act(a), tangents t -> act'(a) * t.
+__global__ void fwdmode_act_kernel(float* a, int d_out, int batch, int ntang, int act, const float* beta) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)d_out * batch) return;
+  const int m = i / batch, b = i - (long)m * batch;
+  const long ld = (long)(ntang + 1) * batch;
+  float* row = a + (long)m * ld;
+  const float z = row[b];
+  float y, dz;
+  if (act == ACT_SWISH) {
+    const float sp = softplus_f(*beta);
+    y = swish_f(z, sp);
+    dz = swish_d(z, sp);
+  } else if (act == ACT_SIN) {
+    y = sinact_f(z);
+    dz = sinact_d(z);
+  } else {
+    y = z;
+    dz = 1.f;
+  }
+  row[b] = y;
+  for (int j = 1; j <= ntang; ++j) row[(long)j * batch + b] *= dz;
+}
+int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, int act, const float* beta,
+                       hipStream_t s) {
+  (void)deriv;
+  const long n = (long)d_out * batch;
+  hipLaunchKernelGGL(fwdmode_act_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, d_out, batch, ntang, act, beta);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// power-series combine: tr_k[b] = (float) sum_chunks partial[k][b][c];  out[b] = sum_k fl(c_k * tr_k)
+// accumulated in fp32 in k order like `logdetgrad = logdetgrad + delta` (implicit_block.py:421-426).
+// ------------------------------------------------------------------------------------------
+struct CoeffTable {
+  float c[128];
+};
+__global__ void series_combine_kernel(const double* partials, CoeffTable ct, int n_terms, int batch, int nchunk,
+                                      float* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  float acc = 0.f;
+  for (int k = 0; k < n_terms; ++k) {
+    double s = 0.0;
+    const double* p = partials + ((long)k * batch + b) * nchunk;
+    for (int c = 0; c < nchunk; ++c) s += p[c];
+    acc = acc + ct.c[k] * (float)s;
+  }
+  out[b] = acc;
+}
+int launch_series_combine(const double* partials, const float* coeff_host, int n_terms, int batch, int nchunk,
+                          float* out, hipStream_t s) {
+  if (n_terms > 128) return INF_ERR_UNSUPPORTED;
+  CoeffTable ct;
+  for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
+  hipLaunchKernelGGL(series_combine_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, partials, ct, n_terms, batch,
+                     nchunk, out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+}  // namespace inf

@@ -1,0 +1,251 @@
+"""ctypes binding of libinflow.so (include/inflow.h) + the per-net plan cache.
+
+The drop-in modules hand raw device pointers of their parameters to the engine; the engine
+keeps Lipschitz-normalised, MFMA-packed copies (inf_net_refresh) that are rebuilt only when a
+parameter tensor changes (tracked through torch's version counters / storage pointers).
+Nothing here computes: every numerical op of the hot path runs in libinflow.so, and a missing
+library raises instead of falling back to PyTorch.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libinflow.so')
+
+INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
+
+
+class LayerDesc(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int), ('cin', ctypes.c_int), ('cout', ctypes.c_int), ('ksize', ctypes.c_int),
+                ('weight', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('u', ctypes.c_void_p),
+                ('v', ctypes.c_void_p), ('coeff', ctypes.c_float), ('beta', ctypes.c_void_p)]
+
+
+class NetDesc(ctypes.Structure):
+    _fields_ = [('n_layers', ctypes.c_int), ('layers', ctypes.POINTER(LayerDesc)), ('channels', ctypes.c_int),
+                ('height', ctypes.c_int), ('width', ctypes.c_int)]
+
+
+class BroydenStats(ctypes.Structure):
+    _fields_ = [('nstep', ctypes.c_int), ('lowest_step', ctypes.c_int), ('prot_break', ctypes.c_int),
+                ('n_trace', ctypes.c_int), ('trace', ctypes.c_double * 64), ('diff', ctypes.c_double),
+                ('eps', ctypes.c_double), ('fixed_point_iters', ctypes.c_int)]
+
+    def as_dict(self, threshold):
+        return {'nstep': self.nstep, 'tnstep': self.nstep, 'lowest_step': self.lowest_step,
+                'diff': self.diff, 'prot_break': bool(self.prot_break),
+                'trace': [self.trace[i] for i in range(self.n_trace)], 'eps': self.eps,
+                'threshold': threshold, 'fixed_point_iters': self.fixed_point_iters}
+
+
+class HipError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_SIGS = {
+    'inf_version': (ctypes.c_int, []),
+    'inf_status_string': (ctypes.c_char_p, [ctypes.c_int]),
+    'inf_last_hip_error': (ctypes.c_int, []),
+    'inf_net_create': (ctypes.c_int, [ctypes.POINTER(NetDesc), ctypes.POINTER(_P)]),
+    'inf_net_destroy': (ctypes.c_int, [_P]),
+    'inf_net_refresh': (ctypes.c_int, [_P, _P]),
+    'inf_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int]),
+    'inf_net_forward': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_net_vjp': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_root_find': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                     ctypes.POINTER(BroydenStats), _P, _P, ctypes.c_size_t, _P]),
+    'inf_imblock_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                           ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
+    'inf_broyden_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    'inf_broyden_update': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logdet_series': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
+                                         ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logdet_neumann': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
+                                          ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logdet_exact': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logit_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_float, _P]),
+    'inf_actnorm_forward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    'inf_squeeze2': (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
+    'inf_normal_logprob': (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
+    'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
+}
+EXPORTS = tuple(_SIGS)
+
+
+def load(path=LIB_PATH):
+    """Load libinflow.so once.  Raises if it was not built (no silent fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise HipError('libinflow.so is not built (%s); run __graft_entry__.build()' % path)
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+        return _lib
+
+
+def check(status, what):
+    if status != 0:
+        lib = load()
+        msg = lib.inf_status_string(status).decode()
+        raise HipError('%s failed: %s (status %d, hip error %d)' % (what, msg, status, lib.inf_last_hip_error()))
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(t, who):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise HipError('%s runs on the MI355X engine (libinflow.so) and needs a HIP device tensor; got %s'
+                       % (who, 'a CPU tensor' if isinstance(t, torch.Tensor) else type(t).__name__))
+    if t.dtype != torch.float32:
+        raise HipError('%s: fp32 tensors only (got %s)' % (who, t.dtype))
+
+
+# ---------------------------------------------------------------------------------------------
+# workspace: one growable uint8 buffer per device, stream-ordered reuse
+# ---------------------------------------------------------------------------------------------
+_ws = {}
+
+
+def workspace(device, nbytes):
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(int(nbytes * 1.1) + 4096, dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+# ---------------------------------------------------------------------------------------------
+# native nets
+# ---------------------------------------------------------------------------------------------
+class NativeNet:
+    """An InfNet built from a flat list of (kind, module) entries of an nn.Sequential."""
+
+    def __init__(self, entries, shape, device):
+        self.lib = load()
+        self.device = device
+        self.shape = tuple(shape)                  # (C, H, W) or (d,)
+        self._tensors = []
+        descs = []
+        for kind, m in entries:
+            d = LayerDesc()
+            if kind in (INF_LAYER_CONV, INF_LAYER_LINEAR):
+                w = m.weight
+                d.kind = kind
+                d.cin, d.cout = int(w.shape[1]), int(w.shape[0])
+                d.ksize = int(w.shape[2]) if kind == INF_LAYER_CONV else 1
+                d.weight, d.bias, d.u, d.v = ptr(w), ptr(m.bias), ptr(m.u), ptr(m.v)
+                d.coeff = float(m.coeff)
+                self._tensors += [w, m.bias, m.u, m.v]
+            else:
+                d.kind = kind
+                if kind == INF_ACT_SWISH:
+                    d.beta = ptr(m.beta)
+                    self._tensors.append(m.beta)
+            descs.append(d)
+        arr = (LayerDesc * len(descs))(*descs)
+        nd = NetDesc()
+        nd.n_layers = len(descs)
+        nd.layers = arr
+        if len(self.shape) == 3:
+            nd.channels, nd.height, nd.width = self.shape
+        else:
+            nd.channels, nd.height, nd.width = self.shape[0], 1, 1
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(self.lib.inf_net_create(ctypes.byref(nd), ctypes.byref(h)), 'inf_net_create')
+        self.handle = h
+        self._stamp = None
+        self.ptrs = self.current_ptrs()
+
+    def current_ptrs(self):
+        return tuple(t.data_ptr() for t in self._tensors)
+
+    def stamp(self):
+        return tuple((t.data_ptr(), t._version) for t in self._tensors)
+
+    def refresh_if_needed(self, stream):
+        st = self.stamp()
+        if st != self._stamp:
+            check(self.lib.inf_net_refresh(self.handle, stream), 'inf_net_refresh')
+            self._stamp = st
+
+    def ws_bytes(self, batch, threshold=1):
+        return int(self.lib.inf_workspace_bytes(self.handle, int(batch), int(threshold)))
+
+    def __del__(self):
+        try:
+            if getattr(self, 'handle', None) and _lib is not None:
+                _lib.inf_net_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def net_entries(seq):
+    """Flatten an nn.Sequential of InducedNorm layers + activations into engine layer kinds.
+    Returns None when the net holds a module the engine does not implement."""
+    from ..layers.base import lipschitz_ops as lo
+    from ..layers.base import nonlin
+    entries = []
+    mods = list(seq.children()) if isinstance(seq, torch.nn.Sequential) else None
+    if mods is None:
+        inner = getattr(seq, 'nnet', None)           # FCNet wrapper (implicit_flow.FCNet)
+        if isinstance(inner, torch.nn.Sequential):
+            mods = list(inner.children())
+        else:
+            return None
+    for m in mods:
+        if isinstance(m, lo.InducedNormConv2d):
+            if tuple(m.stride) != (1, 1) or tuple(m.padding) != (m.kernel_size[0] // 2,) * 2 or m.bias is None:
+                return None
+            entries.append((INF_LAYER_CONV, m))
+        elif isinstance(m, lo.InducedNormLinear):
+            if m.bias is None:
+                return None
+            entries.append((INF_LAYER_LINEAR, m))
+        elif isinstance(m, nonlin.Swish):
+            entries.append((INF_ACT_SWISH, m))
+        elif isinstance(m, nonlin.Sin):
+            entries.append((INF_ACT_SIN, m))
+        else:
+            return None
+    return entries
+
+
+def native_net(module, shape, device):
+    """Cached NativeNet for `module` acting on per-sample `shape` on `device`."""
+    cache = module.__dict__.setdefault('_inf_native', {})
+    key = (torch.device(device).index, tuple(shape))
+    net = cache.get(key) or cache.get((key[0], (int(torch.Size(shape).numel()),)))
+    if net is not None and net.current_ptrs() == net.ptrs:
+        return net
+    entries = net_entries(module)
+    if entries is not None and entries and all(k != INF_LAYER_CONV for k, _ in entries):
+        shape = (int(torch.Size(shape).numel()),)     # fc nets act on the flattened sample
+        key = (key[0], tuple(shape))
+    if entries is None:
+        raise HipError('net %s is not supported by the MI355X engine (supported: nn.Sequential of '
+                       'InducedNormConv2d (stride 1, k in {1,3}) / InducedNormLinear with Swish / Sin)'
+                       % type(module).__name__)
+    net = NativeNet(entries, shape, device)
+    cache[key] = net
+    return net

@@ -1,0 +1,228 @@
+"""Lipschitz-capped conv / linear layers (reference: lib/layers/base/mixed_lipschitz.py,
+factories lib/layers/base/lipschitz.py:510-531).
+
+Each layer keeps the reference's parameters and buffers (``weight, bias, scale, u, v`` and for
+convs ``initialized, spatial_dims``) so state dicts and checkpoints are interchangeable.  The
+effective weight is ``W / max(1, u.(W v) / coeff)``.  On the hot path the MI355X engine computes
+that scale and repacks the weights itself (``inf_net_refresh``); the methods here maintain u/v
+(power iteration, ``update=True``) and give the plain-tensor forward for direct calls.
+
+Only the domain = codomain = 2 (spectral) case that every run_*.sh config selects is provided.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.nn.init as init
+
+__all__ = ['InducedNormConv2d', 'InducedNormLinear', 'get_conv2d', 'get_linear']
+
+
+def _unit(t):
+    return F.normalize(t, p=2, dim=0)
+
+
+def _power_iterate(apply_w, apply_wt, u, v, max_itrs, atol, rtol):
+    """u <- W v / |.|, v <- W^T u / |.| until both move less than atol + rtol*max (mixed_lipschitz.py:295-310,348-368)."""
+    for _ in range(max_itrs):
+        u_prev, v_prev = u, v
+        u = _unit(apply_w(v))
+        v = _unit(apply_wt(u))
+        if atol is not None and rtol is not None:
+            du = torch.norm(u - u_prev) / (u.nelement() ** 0.5)
+            dv = torch.norm(v - v_prev) / (v.nelement() ** 0.5)
+            if du < atol + rtol * torch.max(u) and dv < atol + rtol * torch.max(v):
+                break
+    return u, v
+
+
+def _iteration_budget(n_iterations, atol, rtol):
+    if n_iterations is None and (atol is None or rtol is None):
+        raise ValueError('Need one of n_iteration or (atol, rtol).')
+    return n_iterations if n_iterations is not None else 200
+
+
+class InducedNormLinear(nn.Module):
+
+    def __init__(self, in_features, out_features, bias=True, coeff=0.97, domain=2, codomain=2, n_iterations=None,
+                 atol=None, rtol=None, zero_init=False, **unused_kwargs):
+        super().__init__()
+        if domain != 2 or codomain != 2:
+            raise NotImplementedError('only the spectral (2 -> 2) induced norm is provided')
+        self.in_features, self.out_features = in_features, out_features
+        self.coeff, self.n_iterations, self.atol, self.rtol = coeff, n_iterations, atol, rtol
+        self.domain, self.codomain = domain, codomain
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
+        if not bias:
+            self.register_parameter('bias', None)
+        init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if zero_init:
+            self.weight.data.div_(1000)
+        if self.bias is not None:
+            bound = 1 / math.sqrt(in_features)
+            init.uniform_(self.bias, -bound, bound)
+        self.register_buffer('scale', torch.tensor(0.))
+        self.register_buffer('u', _unit(self.weight.new_empty(out_features).normal_(0, 1)))
+        self.register_buffer('v', _unit(self.weight.new_empty(in_features).normal_(0, 1)))
+        with torch.no_grad():
+            self.compute_weight(True, n_iterations=200, atol=None, rtol=None)
+
+    def compute_weight(self, update=True, n_iterations=None, atol=None, rtol=None):
+        W = self.weight
+        if update:
+            n_iterations = self.n_iterations if n_iterations is None else n_iterations
+            atol = self.atol if atol is None else atol
+            rtol = self.rtol if rtol is None else atol          # the reference reads atol here too
+            itrs = _iteration_budget(n_iterations, atol, rtol)
+            with torch.no_grad():
+                tol = (atol, rtol) if n_iterations is None else (None, None)
+                u, v = _power_iterate(lambda t: torch.mv(W, t), lambda t: torch.mv(W.t(), t), self.u, self.v,
+                                      itrs, *tol)
+                self.u.copy_(u)
+                self.v.copy_(v)
+        sigma = torch.dot(self.u, torch.mv(W, self.v))
+        with torch.no_grad():
+            self.scale.copy_(sigma)
+        return W / torch.max(torch.ones(1, device=W.device), sigma / self.coeff)
+
+    def compute_one_iter(self):
+        W = self.weight.detach()
+        u = _unit(torch.mv(W, self.v))
+        v = _unit(torch.mv(W.t(), u))
+        return torch.dot(u, torch.mv(W, v))
+
+    def forward(self, x):
+        return F.linear(x, self.compute_weight(update=False), self.bias)
+
+    def extra_repr(self):
+        return 'in_features={}, out_features={}, bias={}, coeff={}, n_iters={}, atol={}, rtol={}'.format(
+            self.in_features, self.out_features, self.bias is not None, self.coeff, self.n_iterations, self.atol,
+            self.rtol)
+
+
+class InducedNormConv2d(nn.Module):
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, padding, bias=True, coeff=0.97, domain=2,
+                 codomain=2, n_iterations=None, atol=None, rtol=None, **unused_kwargs):
+        super().__init__()
+        if domain != 2 or codomain != 2:
+            raise NotImplementedError('only the spectral (2 -> 2) induced norm is provided')
+        pair = lambda a: tuple(a) if isinstance(a, (tuple, list)) else (a, a)
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = pair(kernel_size), pair(stride), pair(padding)
+        self.coeff, self.n_iterations, self.atol, self.rtol = coeff, n_iterations, atol, rtol
+        self.domain, self.codomain = domain, codomain
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels, *self.kernel_size))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_channels))
+        else:
+            self.register_parameter('bias', None)
+        init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(in_channels * self.kernel_size[0] * self.kernel_size[1])
+            init.uniform_(self.bias, -bound, bound)
+        self.register_buffer('initialized', torch.tensor(0))
+        self.register_buffer('spatial_dims', torch.tensor([1., 1.]))
+        self.register_buffer('scale', torch.tensor(0.))
+        self.register_buffer('u', self.weight.new_empty(out_channels))
+        self.register_buffer('v', self.weight.new_empty(in_channels))
+
+    # u/v are sized by the first input's spatial dims; accept checkpoints whatever the current size
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        for name in ('u', 'v'):
+            key = prefix + name
+            if key in state_dict and state_dict[key].shape != getattr(self, name).shape:
+                setattr(self, name, getattr(self, name).new_empty(state_dict[key].shape))
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+    @property
+    def is_1x1(self):
+        return self.kernel_size == (1, 1)
+
+    def _hw(self):
+        return int(self.spatial_dims[0].item()), int(self.spatial_dims[1].item())
+
+    def _conv_ops(self, W):
+        c = self.in_channels
+        h, w = self._hw()
+        fwd = lambda t: F.conv2d(t.view(1, c, h, w), W, stride=self.stride, padding=self.padding).reshape(-1)
+        shape = F.conv2d(torch.zeros(1, c, h, w, device=W.device, dtype=W.dtype), W, stride=self.stride,
+                         padding=self.padding).shape
+        bwd = lambda t: F.conv_transpose2d(t.view(shape), W, stride=self.stride, padding=self.padding).reshape(-1)
+        return fwd, bwd, shape
+
+    def _initialize_u_v(self):
+        """mixed_lipschitz.py:195-239 (spectral case): random unit u/v, then power iteration."""
+        with torch.no_grad():
+            if self.is_1x1:
+                self.u = _unit(self.weight.new_empty(self.out_channels).normal_(0, 1))
+                self.v = _unit(self.weight.new_empty(self.in_channels).normal_(0, 1))
+            else:
+                h, w = self._hw()
+                self.v = _unit(self.weight.new_empty(self.in_channels * h * w).normal_(0, 1))
+                _, _, shape = self._conv_ops(self.weight)
+                self.u = _unit(self.weight.new_empty(int(torch.Size(shape).numel())).normal_(0, 1))
+            self.initialized.fill_(1)
+            self.compute_weight(True)
+
+    def compute_weight(self, update=True, n_iterations=None, atol=None, rtol=None):
+        if not self.initialized:
+            self._initialize_u_v()
+        n_iterations = self.n_iterations if n_iterations is None else n_iterations
+        atol = self.atol if atol is None else atol
+        rtol = self.rtol if rtol is None else atol              # the reference reads atol here too
+        itrs = _iteration_budget(n_iterations, atol, rtol)
+        W = self.weight
+        if self.is_1x1:
+            Wm = W.view(self.out_channels, self.in_channels)
+            fwd, bwd = (lambda t: torch.mv(Wm, t)), (lambda t: torch.mv(Wm.t(), t))
+        else:
+            fwd, bwd, _ = self._conv_ops(W)
+        if update:
+            with torch.no_grad():
+                tol = (atol, rtol) if n_iterations is None else (None, None)
+                u, v = _power_iterate(fwd, bwd, self.u.view(-1), self.v.view(-1), itrs, *tol)
+                self.u.copy_(u.view_as(self.u))
+                self.v.copy_(v.view_as(self.v))
+        sigma = torch.dot(self.u.view(-1), fwd(self.v))
+        with torch.no_grad():
+            self.scale.copy_(sigma)
+        return W / torch.max(torch.ones(1, device=W.device), sigma / self.coeff)
+
+    def compute_one_iter(self):
+        if not self.initialized:
+            raise ValueError('Layer needs to be initialized first.')
+        W = self.weight.detach()
+        if self.is_1x1:
+            Wm = W.view(self.out_channels, self.in_channels)
+            fwd, bwd = (lambda t: torch.mv(Wm, t)), (lambda t: torch.mv(Wm.t(), t))
+        else:
+            fwd, bwd, _ = self._conv_ops(W)
+        u = _unit(fwd(self.v.view(-1)))
+        v = _unit(bwd(u))
+        return torch.dot(u, fwd(v))
+
+    def forward(self, x):
+        if not self.initialized:
+            self.spatial_dims.copy_(torch.tensor(x.shape[2:4]).to(self.spatial_dims))
+        return F.conv2d(x, self.compute_weight(update=False), self.bias, self.stride, self.padding, 1, 1)
+
+    def extra_repr(self):
+        return '{}, {}, kernel_size={}, stride={}, padding={}, coeff={}, n_iters={}, atol={}, rtol={}'.format(
+            self.in_channels, self.out_channels, self.kernel_size, self.stride, self.padding, self.coeff,
+            self.n_iterations, self.atol, self.rtol)
+
+
+def get_linear(in_features, out_features, bias=True, coeff=0.97, domain=None, codomain=None, **kwargs):
+    """lipschitz.py:510-518 with domain = codomain = 2 -> InducedNormLinear."""
+    return InducedNormLinear(in_features, out_features, bias, coeff, 2 if domain is None else domain,
+                             2 if codomain is None else codomain, **kwargs)
+
+
+def get_conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=True, coeff=0.97, domain=None,
+               codomain=None, **kwargs):
+    """lipschitz.py:521-531 with domain = codomain = 2 -> InducedNormConv2d."""
+    return InducedNormConv2d(in_channels, out_channels, kernel_size, stride, padding, bias, coeff,
+                             2 if domain is None else domain, 2 if codomain is None else codomain, **kwargs)

@@ -1,0 +1,218 @@
+"""imBlock — drop-in for the reference's implicit block (lib/layers/implicit_block.py:103-355).
+
+Same constructor, attributes, buffers and state-dict keys; ``forward(x, logpx=None,
+restore=False)`` and ``inverse(z, logpy=None)`` return the same values.  The work runs on the
+MI355X engine:
+
+  * root solve + z recompute  -> inf_imblock_forward  (RootFind/broyden, :68-80 + :226-227)
+  * inverse                   -> inf_root_find        (:236-243)
+  * power-series log-det      -> inf_logdet_series    (basic_logdet_estimator, :418-426)
+  * Neumann surrogate value   -> inf_logdet_neumann   (:429-438, train mode)
+  * exact small log-det       -> inf_logdet_exact     (d <= 10 in eval / brute_force, :249-260)
+
+Host work is only what the reference does on the host: the series-length draw (numpy global
+RNG) and, in the default ``'reference'`` probe mode, the Rademacher probes from torch's CPU
+generator in the reference's order (vareps_x, then vareps_z), so seeded runs replay exactly.
+``set_probe_mode('device')`` draws the probes on the GPU instead (counter-based generator).
+
+Training (implicit backward, mem-efficient estimator gradients) is not implemented yet; a
+train-mode forward that needs gradients raises instead of returning a graph-less value.
+"""
+import copy
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _hip
+from . import solvers
+
+__all__ = ['imBlock', 'set_probe_mode']
+
+_PROBES = {'mode': 'reference', 'seed': 0, 'offset': 0}
+
+
+def set_probe_mode(mode, seed=0):
+    """'reference' (replay the reference's CPU RNG stream) or 'device' (engine RNG)."""
+    if mode not in ('reference', 'device'):
+        raise ValueError(mode)
+    _PROBES.update(mode=mode, seed=int(seed), offset=0)
+
+
+def _probes(shape, device):
+    out = solvers.rademacher_probes(shape, device, _PROBES['mode'], _PROBES['seed'], _PROBES['offset'])
+    _PROBES['offset'] += int(np.prod(shape))
+    return out
+
+
+def _uninitialised_convs(net):
+    return any(getattr(m, 'initialized', 1) == 0 for m in net.modules() if hasattr(m, 'spatial_dims'))
+
+
+class imBlock(nn.Module):
+
+    def __init__(self, nnet_x, nnet_z, geom_p=0.5, lamb=2., n_power_series=None, exact_trace=False,
+                 brute_force=False, n_samples=1, n_exact_terms=2, n_exact_terms_test=20, n_dist='geometric',
+                 neumann_grad=True, grad_in_forward=True, eps_forward=1e-6, eps_backward=1e-10, eps_sample=1e-5,
+                 threshold=30):
+        super().__init__()
+        self.nnet_x = nnet_x
+        self.nnet_z = nnet_z
+        # frozen copies, kept for state-dict compatibility (implicit_block.py:136-141)
+        self.nnet_x_copy = copy.deepcopy(nnet_x)
+        self.nnet_z_copy = copy.deepcopy(nnet_z)
+        for p in list(self.nnet_x_copy.parameters()) + list(self.nnet_z_copy.parameters()):
+            p.requires_grad_(False)
+        self.n_dist = n_dist
+        # geom_p is a plain tensor (not registered) in the reference (quirk, :144)
+        self.geom_p = torch.tensor(float(np.log(geom_p) - np.log(1. - geom_p))).float()
+        self.lamb = nn.Parameter(torch.tensor(float(lamb)))
+        self.n_samples = n_samples
+        self.n_power_series = n_power_series
+        self.exact_trace = exact_trace
+        self.brute_force = brute_force
+        self.n_exact_terms = n_exact_terms
+        self.n_exact_terms_test = n_exact_terms_test
+        self.grad_in_forward = grad_in_forward
+        self.neumann_grad = neumann_grad
+        self.eps_forward = eps_forward
+        self.eps_backward = eps_backward
+        self.eps_sample = eps_sample
+        self.threshold = threshold
+        self.register_buffer('last_n_samples', torch.zeros(self.n_samples))
+        self.register_buffer('last_firmom', torch.zeros(1))
+        self.register_buffer('last_secmom', torch.zeros(1))
+        self.last_broyden = None
+
+    # ---------------------------------------------------------------------------------------
+    def _native(self, t):
+        _hip.require_device(t, 'imBlock')
+        shape = t.shape[1:]
+        for net in (self.nnet_x, self.nnet_z):
+            if _uninitialised_convs(net):            # lazy u/v sizing on first use (mixed_lipschitz.py:389)
+                with torch.no_grad():
+                    net(t[:1])
+        stream = _hip.stream_of(t)
+        nets = []
+        for net in (self.nnet_x, self.nnet_z):
+            n = _hip.native_net(net, shape, t.device)
+            n.refresh_if_needed(stream)
+            nets.append(n)
+        return nets[0], nets[1], stream
+
+    def _check_grad(self, *ts):
+        if self.training and torch.is_grad_enabled() and (
+                any(t.requires_grad for t in ts) or any(p.requires_grad for p in self.parameters())):
+            raise NotImplementedError('imBlock training backward (implicit_block.py:165-217, :373-415) is not '
+                                      'implemented on the MI355X engine yet; run train-mode forwards under '
+                                      'torch.no_grad()')
+
+    def _root(self, net_f, net_e, y, eps, stream, forward):
+        lib = _hip.load()
+        y = y.contiguous()
+        B = y.shape[0]
+        T = int(self.threshold)
+        ws = _hip.workspace(y.device, max(net_f.ws_bytes(B, T), net_e.ws_bytes(B, T)))
+        out = torch.empty_like(y)
+        st = _hip.BroydenStats()
+        if forward:
+            rc = lib.inf_imblock_forward(net_e.handle, net_f.handle, _hip.ptr(y), _hip.ptr(out), B, T, float(eps),
+                                         ctypes.byref(st), _hip.ptr(ws), ws.numel(), stream)
+            _hip.check(rc, 'inf_imblock_forward')
+        else:
+            rc = lib.inf_root_find(net_f.handle, net_e.handle, _hip.ptr(y), _hip.ptr(out), B, T, float(eps),
+                                   ctypes.byref(st), None, _hip.ptr(ws), ws.numel(), stream)
+            _hip.check(rc, 'inf_root_find')
+        self.last_broyden = st.as_dict(T)
+        return out
+
+    # ---------------------------------------------------------------------------------------
+    def forward(self, x, logpx=None, restore=False):
+        self._check_grad(x)
+        if restore:
+            with torch.no_grad():
+                self.nnet_x_copy(x)
+                self.nnet_z_copy(x)
+        nx, nz, stream = self._native(x)
+        with torch.no_grad():
+            z = self._root(nz, nx, x, self.eps_forward, stream, forward=True)
+        if self.training:       # keep the frozen copies in step (implicit_block.py:228-229)
+            self.nnet_x_copy.load_state_dict(self.nnet_x.state_dict())
+            self.nnet_z_copy.load_state_dict(self.nnet_z.state_dict())
+        if logpx is None:
+            return z
+        return z, logpx - self._logdetgrad(z, x)
+
+    def inverse(self, z, logpy=None):
+        self._check_grad(z)
+        nx, nz, stream = self._native(z)
+        with torch.no_grad():
+            x = self._root(nx, nz, z, self.eps_sample, stream, forward=False)
+        if logpy is None:
+            return x
+        return x, logpy + self._logdetgrad(z, x)
+
+    # ---------------------------------------------------------------------------------------
+    def _series_plan(self):
+        """Series length and coefficient function (implicit_block.py:261-289)."""
+        if self.n_dist == 'geometric':
+            param = torch.sigmoid(self.geom_p).item()
+        elif self.n_dist == 'poisson':
+            param = self.lamb.item()
+        else:
+            raise ValueError(self.n_dist)
+        if self.training and self.n_power_series is not None:
+            return self.n_power_series, (lambda k: 1.), None
+        n_exact = self.n_exact_terms if self.training else self.n_exact_terms_test
+        return solvers.series_coefficients(self.n_dist, param, n_exact, self.n_samples)
+
+    def _logdetgrad(self, z, x):
+        """log|det dz/dx| per sample, shape (B, 1) (implicit_block.py:245-350)."""
+        lib = _hip.load()
+        nx, nz, stream = self._native(x)
+        B = x.shape[0]
+        if (self.brute_force or not self.training) and x.dim() == 2 and x.shape[1] <= 10:
+            out = torch.empty(2, B, device=x.device)
+            ws = _hip.workspace(x.device, max(nx.ws_bytes(B), nz.ws_bytes(B)))
+            for i, (net, t) in enumerate(((nx, x), (nz, z))):
+                _hip.check(lib.inf_logdet_exact(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(out[i]), B,
+                                                _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_exact')
+            return (out[0] - out[1]).view(-1, 1)
+        if self.exact_trace:
+            raise NotImplementedError('exact_trace=True (batch_jacobian power series, implicit_block.py:323-343) '
+                                      'is not implemented on the MI355X engine')
+        n_ps, coeff_fn, ns = self._series_plan()
+        vareps_x = _probes(x.shape, x.device)
+        vareps_z = _probes(z.shape, z.device)
+        ws = _hip.workspace(x.device, max(nx.ws_bytes(B), nz.ws_bytes(B)))
+        out = torch.empty(2, B, device=x.device)
+        if self.training and self.neumann_grad:
+            nco = np.zeros(n_ps + 1, dtype=np.float32)
+            nco[0] = 1.
+            for k in range(1, n_ps + 1):
+                nco[k] = (-1) ** k * coeff_fn(k)
+            carr = nco.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+            for i, (net, t, e) in enumerate(((nx, x, vareps_x), (nz, z, vareps_z))):
+                _hip.check(lib.inf_logdet_neumann(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(e), carr, n_ps,
+                                                  _hip.ptr(out[i]), B, _hip.ptr(ws), ws.numel(), stream),
+                           'inf_logdet_neumann')
+        else:
+            co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+            carr = co.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+            for i, (net, t, e) in enumerate(((nx, x, vareps_x), (nz, z, vareps_z))):
+                _hip.check(lib.inf_logdet_series(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(e), carr, n_ps,
+                                                 _hip.ptr(out[i]), B, _hip.ptr(ws), ws.numel(), stream),
+                           'inf_logdet_series')
+        logdetgrad = out[0] - out[1]
+        self.last_n_power_series = n_ps
+        if self.training and self.n_power_series is None:
+            self.last_n_samples.copy_(torch.as_tensor(np.asarray(ns)).to(self.last_n_samples))
+            self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
+            self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
+        return logdetgrad.view(-1, 1)
+
+    def extra_repr(self):
+        return ('dist={}, n_samples={}, n_power_series={}, neumann_grad={}, exact_trace={}, brute_force={}, '
+                'grad_in_forward={}'.format(self.n_dist, self.n_samples, self.n_power_series, self.neumann_grad,
+                                            self.exact_trace, self.brute_force, self.grad_in_forward))

@@ -1,0 +1,116 @@
+"""iResBlock — drop-in for the reference's residual-flow block (lib/layers/iresblock.py:13-169).
+
+y = x + g(x); log|det(I + J_g)| by the same power-series estimator as imBlock but with
+Gaussian probes (iresblock.py:129) and 20 hard-coded exact terms in eval (:121-123); exact
+2x2 determinant for 2-D inputs (:85-94).  Runs on the MI355X engine like imBlock (one net
+instead of two).  Unlike the reference it also accepts ``restore=`` so it can sit inside
+SequentialFlow (the reference's raises TypeError there).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _hip
+from . import solvers
+
+__all__ = ['iResBlock']
+
+
+class iResBlock(nn.Module):
+
+    def __init__(self, nnet, geom_p=0.5, lamb=2., n_power_series=None, exact_trace=False, brute_force=False,
+                 n_samples=1, n_exact_terms=2, n_dist='geometric', neumann_grad=True, grad_in_forward=False):
+        super().__init__()
+        self.nnet = nnet
+        self.n_dist = n_dist
+        self.geom_p = nn.Parameter(torch.tensor(np.log(geom_p) - np.log(1. - geom_p)))
+        self.lamb = nn.Parameter(torch.tensor(lamb))
+        self.n_samples = n_samples
+        self.n_power_series = n_power_series
+        self.exact_trace = exact_trace
+        self.brute_force = brute_force
+        self.n_exact_terms = n_exact_terms
+        self.grad_in_forward = grad_in_forward
+        self.neumann_grad = neumann_grad
+        self.register_buffer('last_n_samples', torch.zeros(self.n_samples))
+        self.register_buffer('last_firmom', torch.zeros(1))
+        self.register_buffer('last_secmom', torch.zeros(1))
+
+    def _native(self, x):
+        _hip.require_device(x, 'iResBlock')
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError('iResBlock training backward is not implemented on the MI355X engine')
+        net = _hip.native_net(self.nnet, x.shape[1:], x.device)
+        stream = _hip.stream_of(x)
+        net.refresh_if_needed(stream)
+        return net, stream
+
+    def _g(self, net, x, stream):
+        B = x.shape[0]
+        ws = _hip.workspace(x.device, net.ws_bytes(B))
+        y = torch.empty_like(x)
+        _hip.check(_hip.load().inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
+                                               stream), 'inf_net_forward')
+        return y
+
+    def forward(self, x, logpx=None, restore=False):
+        x = x.contiguous()
+        net, stream = self._native(x)
+        with torch.no_grad():
+            g = self._g(net, x, stream)
+            if logpx is None:
+                return x + g
+            return x + g, logpx - self._logdetgrad(net, x, stream)
+
+    def inverse(self, y, logpy=None):
+        y = y.contiguous()
+        net, stream = self._native(y)
+        with torch.no_grad():
+            # x <- y - g(x) until converged (iresblock.py:69-79)
+            x, x_prev = y - self._g(net, y, stream), y
+            tol = 1e-5 + y.abs() * 1e-5
+            i = 0
+            while not torch.all((x - x_prev) ** 2 / tol < 1):
+                x, x_prev = y - self._g(net, x, stream), x
+                i += 1
+                if i > 1000:
+                    break
+            if logpy is None:
+                return x
+            return x, logpy + self._logdetgrad(net, x, stream)
+
+    def _logdetgrad(self, net, x, stream):
+        lib = _hip.load()
+        B = x.shape[0]
+        ws = _hip.workspace(x.device, net.ws_bytes(B))
+        out = torch.empty(B, device=x.device)
+        if (self.brute_force or not self.training) and x.dim() == 2 and x.shape[1] == 2:
+            _hip.check(lib.inf_logdet_exact(net.handle, _hip.ptr(x), _hip.ptr(out), B, _hip.ptr(ws), ws.numel(),
+                                            stream), 'inf_logdet_exact')
+            return out.view(-1, 1)
+        if self.exact_trace:
+            raise NotImplementedError('exact_trace=True is not implemented on the MI355X engine')
+        param = torch.sigmoid(self.geom_p).item() if self.n_dist == 'geometric' else self.lamb.item()
+        if self.training and self.n_power_series is not None:
+            n_ps, coeff_fn = self.n_power_series, (lambda k: 1.)
+        else:
+            n_exact = self.n_exact_terms if self.training else 20
+            n_ps, coeff_fn, _ = solvers.series_coefficients(self.n_dist, param, n_exact, self.n_samples)
+        vareps = torch.randn_like(x)
+        if self.training and self.neumann_grad:
+            nco = np.array([1.] + [(-1) ** k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+            _hip.check(lib.inf_logdet_neumann(net.handle, _hip.ptr(x), _hip.ptr(vareps),
+                                              nco.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(out),
+                                              B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_neumann')
+        else:
+            co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+            _hip.check(lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(vareps),
+                                             co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(out),
+                                             B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series')
+        return out.view(-1, 1)
+
+    def extra_repr(self):
+        return 'dist={}, n_samples={}, n_power_series={}, neumann_grad={}, exact_trace={}, brute_force={}'.format(
+            self.n_dist, self.n_samples, self.n_power_series, self.neumann_grad, self.exact_trace, self.brute_force)

@@ -97,6 +97,14 @@ int inf_net_vjp(InfNet* net, const float* x, const float* v, float* out, int bat
  * may be NULL) receives the per-sample residual norms of the returned iterate. */
 int inf_root_find(InfNet* net_f, InfNet* net_e, const float* y, float* out, int batch, int threshold, double eps,
                   InfBroydenStats* stats, float* diff_detail, void* ws, size_t ws_bytes, void* stream);
+/* One limited-memory Broyden update for a caller-driven loop (generic broyden(g, x0, ...), broyden.py:
+ * 174-181 + the next line_search step :94-99).  Tensors are (B, d) row-major; U/VT are (T, B, d).
+ * nstep = iterations done so far (>= 1).  Writes update = -H gx, x_next = x + update and
+ * dx_next = x_next - x.  ws >= inf_broyden_workspace_bytes(batch, d, threshold). */
+size_t inf_broyden_workspace_bytes(int batch, int d, int threshold);
+int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, const float* gx, const float* x,
+                       float* update, float* x_next, float* dx_next, int batch, int d, int threshold, int nstep,
+                       void* ws, size_t ws_bytes, void* stream);
 /* imBlock forward value: z* = RootFind(nnet_z, nnet_x, x); z = (nnet_x(x) - nnet_z(z*)) + x
  * (implicit_block.py:226-227). */
 int inf_imblock_forward(InfNet* net_x, InfNet* net_z, const float* x, float* z, int batch, int threshold,

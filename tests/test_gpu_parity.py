@@ -1,0 +1,232 @@
+"""Parity of the MI355X engine (libinflow.so via the drop-in modules) against the oracle (CPU
+restatement) and against the golden vectors produced by the reference itself.
+
+Tolerances (north star: bits/dim within 1e-5 abs of the reference):
+  * bits/dim / nats per batch:        |delta| <= 1e-5
+  * per-sample log p(x):              |delta| <= 2e-3 nats   (=> <= 1e-6 bpd per sample at d=3072)
+  * net forward / VJP / z:            |delta| <= 2e-5 * max(1, |ref|_inf)  (fp32, reordered sums)
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from lib import _hip, synthetic as syn
+from lib.configs import build_flow, imblocks
+from lib.density import image_logpx, tabular_logpx
+from lib.layers import solvers
+from oracle import inflow_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def _model(arch, B):
+    sd = syn.make_state_dict(arch, 0)
+    m = build_flow(arch, B)
+    m.load_state_dict(sd, strict=True)
+    return m.to(DEV).eval(), sd
+
+
+def _close(a, b, rel=2e-5):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = max(1.0, b.abs().max().item())
+    err = (a - b).abs().max().item()
+    assert err <= rel * scale, 'max abs err %g > %g' % (err, rel * scale)
+
+
+def _first_block_net(arch, sd, which='nnet_x', block=0):
+    layout = syn.conv_flow_layout(arch) if arch['kind'] == 'conv' else syn.fc_flow_layout(arch)
+    found = []
+    if arch['kind'] == 'conv':
+        for i, chain in enumerate(layout):
+            for j, (kind, info) in enumerate(chain):
+                if kind == 'imblock':
+                    found.append(('transforms.%d.chain.%d' % (i, j), info))
+    else:
+        found = [('chain.%d' % j, info) for j, (k, info) in enumerate(layout)]
+    prefix, info = found[block]
+    return prefix, info
+
+
+@pytest.mark.parametrize('arch,block', [(syn.CIFAR10_SMALL, 0), (syn.CIFAR10_SMALL, 1), (syn.CIFAR10, 0),
+                                        (syn.CIFAR10, 2), (syn.CIFAR10, 5), (syn.POWER, 0), (syn.TOY, 3)])
+def test_net_forward_and_vjp(arch, block):
+    torch.manual_seed(0)
+    B = 3 if arch['kind'] == 'conv' else 257
+    m, sd = _model(arch, B)
+    blk = imblocks(m)[block]
+    prefix, info = _first_block_net(arch, sd, block=block)
+    shape = info['shape']
+    x = torch.randn(B, *shape) * 0.7
+    v = torch.randn(B, *shape)
+    ref_net = orc.make_net(sd, prefix + '.nnet_x', info['net'], arch['coeff'])
+    xr = x.clone().requires_grad_(True)
+    y_ref = ref_net(xr)
+    vjp_ref = torch.autograd.grad(y_ref, xr, v)[0]
+
+    xd, vd = x.to(DEV), v.to(DEV)
+    net = _hip.native_net(blk.nnet_x, xd.shape[1:], xd.device)
+    stream = _hip.stream_of(xd)
+    net.refresh_if_needed(stream)
+    ws = _hip.workspace(xd.device, net.ws_bytes(B))
+    y = torch.empty_like(xd)
+    _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(xd), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(), stream),
+               'fwd')
+    g = torch.empty_like(xd)
+    _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(xd), _hip.ptr(vd), _hip.ptr(g), B, _hip.ptr(ws), ws.numel(),
+                                   stream), 'vjp')
+    torch.cuda.synchronize()
+    _close(y, y_ref)
+    _close(g, vjp_ref)
+
+
+@pytest.mark.parametrize('arch', [syn.CIFAR10_SMALL, syn.CIFAR10])
+def test_logdet_series_same_probes(arch):
+    B = 2
+    m, sd = _model(arch, B)
+    blk = imblocks(m)[1]
+    prefix, info = _first_block_net(arch, sd, block=1)
+    torch.manual_seed(1)
+    x = torch.randn(B, *info['shape']) * 0.5
+    eps = torch.randint(0, 2, x.shape).float() * 2 - 1
+    n = 22
+    coeff_fn = lambda k: 1.0 if k <= 20 else 1.5
+    ref_net = orc.make_net(sd, prefix + '.nnet_x', info['net'], arch['coeff'])
+    xr = x.clone().requires_grad_(True)
+    ref = orc.basic_logdet_estimator(ref_net(xr), xr, n, eps, coeff_fn)
+    xd, ed = x.to(DEV), eps.to(DEV)
+    net = _hip.native_net(blk.nnet_x, xd.shape[1:], xd.device)
+    stream = _hip.stream_of(xd)
+    net.refresh_if_needed(stream)
+    ws = _hip.workspace(xd.device, net.ws_bytes(B))
+    co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n + 1)], dtype=np.float32)
+    out = torch.empty(B, device=DEV)
+    _hip.check(net.lib.inf_logdet_series(net.handle, _hip.ptr(xd), _hip.ptr(ed),
+                                         co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, _hip.ptr(out), B,
+                                         _hip.ptr(ws), ws.numel(), stream), 'series')
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy(), ref.detach().numpy(), rtol=0, atol=2e-3)
+
+
+def _golden(golden_dir, name):
+    path = os.path.join(golden_dir, name + '.npz')
+    if not os.path.exists(path):
+        pytest.skip('missing fixture ' + name)
+    return np.load(path)
+
+
+@pytest.mark.parametrize('name,arch,train', [
+    ('cifar_small_b4', syn.CIFAR10_SMALL, False),
+    ('cifar_full_b2', syn.CIFAR10, False),
+    ('cifar_full_b8', syn.CIFAR10, False),
+    ('power_eval_b256', syn.POWER, False),
+    ('power_train_b256', syn.POWER, True),
+    ('toy_eval_b64', syn.TOY, False),
+])
+def test_flow_matches_reference_golden(golden_dir, name, arch, train):
+    g = _golden(golden_dir, name)
+    x = torch.from_numpy(g['x']).to(DEV)
+    m, _ = _model(arch, x.shape[0])
+    m.train(train)
+    np.random.seed(int(g['seed']))
+    torch.manual_seed(int(g['seed']))
+    if arch['kind'] == 'conv':
+        loss, logpx, z = image_logpx(m, x, arch['nvals'])
+    else:
+        with torch.no_grad():
+            loss, logpx, z = tabular_logpx(m, x)
+    torch.cuda.synchronize()
+    blocks = imblocks(m)
+    for i, b in enumerate(blocks):
+        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]), 'block %d nstep' % i
+        if 'b%d_n_power_series' % i in g:
+            assert b.last_n_power_series == int(g['b%d_n_power_series' % i][0])
+    assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(z.reshape(z.shape[0], -1).cpu().numpy(), g['z'], rtol=0, atol=2e-4)
+
+
+def test_flow_matches_oracle_small_batch():
+    arch = syn.CIFAR10_SMALL
+    x = syn.image_batch(5, seed=9)
+    m, sd = _model(arch, 5)
+    np.random.seed(3)
+    torch.manual_seed(3)
+    loss, logpx, _ = image_logpx(m, x.to(DEV), arch['nvals'])
+    flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
+    np.random.seed(3)
+    torch.manual_seed(3)
+    ref_loss, ref_logpx, _ = orc.image_bits_per_dim(flow, x, arch['nvals'])
+    assert abs(loss.item() - float(ref_loss)) <= 1e-5
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), ref_logpx.view(-1).numpy(), rtol=0, atol=2e-3)
+
+
+def test_deterministic_and_shard_invariant():
+    """Same inputs -> bitwise same bpd; per-sample logpx of a half batch equals the full batch's rows
+    when the probes are the same (Broyden's global stop can differ only below eps)."""
+    arch = syn.CIFAR10_SMALL
+    x = syn.image_batch(4, seed=1).to(DEV)
+    m, _ = _model(arch, 4)
+    outs = []
+    for _ in range(2):
+        np.random.seed(0)
+        torch.manual_seed(0)
+        outs.append(image_logpx(m, x, 256)[1])
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_inverse_roundtrip():
+    arch = syn.CIFAR10_SMALL
+    m, _ = _model(arch, 3)
+    blk = imblocks(m)[2]
+    x = torch.randn(3, 12, 16, 16, device=DEV) * 0.5
+    with torch.no_grad():
+        z = blk(x)
+        xr = blk.inverse(z)
+    _close(xr, x, rel=1e-4)
+
+
+def test_generic_broyden_linear_system():
+    torch.manual_seed(0)
+    B, d = 4, 40
+    A = torch.randn(B, d, d, device=DEV) * (0.3 / d ** 0.5)
+    b = torch.randn(B, d, device=DEV)
+    # root of g(x) = b - x - A x  (contractive A)
+    g = lambda x: b - x - torch.einsum('bij,bj->bi', A, x)
+    r = solvers.broyden(g, torch.zeros(B, d, device=DEV), 30, 1e-6)
+    x_true = torch.linalg.solve(torch.eye(d, device=DEV) + A, b)
+    _close(r['result'], x_true, rel=1e-4)
+    assert r['nstep'] < 30 and not r['prot_break']
+
+
+def test_glue_kernels_match_formulas():
+    from lib.layers import ActNorm2d, LogitTransform, SqueezeLayer
+    torch.manual_seed(0)
+    x = torch.rand(3, 3, 8, 8, device=DEV) * 0.98 + 0.01
+    lt = LogitTransform(0.05)
+    y, lp = lt(x, torch.zeros(3, 1, device=DEV))
+    s = 0.05 + 0.9 * x
+    _close(y, torch.log(s) - torch.log(1 - s))
+    _close(lp, -(-torch.log(s - s * s) + np.log(0.9)).view(3, -1).sum(1, keepdim=True))
+    an = ActNorm2d(3).to(DEV)
+    with torch.no_grad():
+        an.weight.uniform_(-0.3, 0.3)
+        an.bias.uniform_(-0.3, 0.3)
+        an.initialized.fill_(1)
+    y2, lp2 = an(x, 0)
+    _close(y2, (x + an.bias.view(1, -1, 1, 1)) * torch.exp(an.weight.view(1, -1, 1, 1)))
+    _close(lp2, -(an.weight.sum() * 64).expand(3, 1))
+    sq = SqueezeLayer(2)(x)
+    ref = x.reshape(3, 3, 4, 2, 4, 2).permute(0, 1, 3, 5, 2, 4).reshape(3, 12, 4, 4)
+    assert torch.equal(sq, ref)
+
+
+def test_device_rademacher():
+    p = solvers.rademacher_probes((64, 3072), DEV, mode='device', seed=5)
+    vals = torch.unique(p).cpu().tolist()
+    assert vals == [-1.0, 1.0]
+    assert abs(p.mean().item()) < 0.01

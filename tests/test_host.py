@@ -1,0 +1,95 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol include/inflow.h declares,
+host-side logic (series coefficients, RNG replay order, state-dict layout, net plan extraction),
+and that the product path refuses CPU tensors instead of falling back."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from lib import _hip, synthetic as syn
+from lib.configs import build_flow, imblocks
+from lib.layers import solvers
+from oracle import inflow_oracle as orc
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, 'include', 'inflow.h')).read()
+    return sorted(set(re.findall(r'\b(inf_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_hip.LIB_PATH):
+        pytest.skip('libinflow.so not built (run __graft_entry__.build())')
+    lib = ctypes.CDLL(_hip.LIB_PATH)
+    missing = [s for s in _declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(_declared_symbols()) <= set(_hip.EXPORTS)
+    assert lib.inf_version() >= 1
+
+
+def test_binding_signatures_cover_header():
+    assert set(_declared_symbols()) == set(_hip.EXPORTS)
+
+
+@pytest.mark.parametrize('dist,param,n_exact', [('poisson', 2.0, 20), ('geometric', 0.5, 2), ('poisson', 2.0, 10)])
+def test_series_coefficients_match_oracle(dist, param, n_exact):
+    np.random.seed(123)
+    n1, f1, s1 = solvers.series_coefficients(dist, param, n_exact)
+    np.random.seed(123)
+    logit = float(np.log(param) - np.log(1 - param)) if dist == 'geometric' else 0.0
+    n2, f2, s2 = orc.series_plan(dist, param, logit, n_exact)
+    assert n1 == n2 and list(s1) == list(s2)
+    for k in range(1, n1 + 3):
+        assert f1(k) == f2(k)
+
+
+def test_probe_replay_order_matches_reference_draw():
+    torch.manual_seed(5)
+    a = solvers.rademacher_probes((3, 4, 5), 'cpu', mode='reference')
+    b = solvers.rademacher_probes((3, 4, 5), 'cpu', mode='reference')
+    torch.manual_seed(5)
+    ra = orc.rademacher_like(torch.empty(3, 4, 5))
+    rb = orc.rademacher_like(torch.empty(3, 4, 5))
+    assert torch.equal(a, ra) and torch.equal(b, rb)
+
+
+@pytest.mark.parametrize('arch', [syn.CIFAR10_SMALL, syn.POWER, syn.TOY])
+def test_state_dict_layout_matches_reference_keys(arch):
+    sd = syn.make_state_dict(arch, 0)
+    m = build_flow(arch, 4)
+    assert set(m.state_dict()) == set(sd)
+    m.load_state_dict(sd, strict=True)
+    assert len(imblocks(m)) == (sum(arch['n_blocks']) if arch['kind'] == 'conv' else arch['n_blocks'])
+
+
+def test_synthetic_generator_is_deterministic():
+    a = syn.make_state_dict(syn.POWER, 3)
+    b = syn.make_state_dict(syn.POWER, 3)
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    x1, x2 = syn.image_batch(2, seed=1), syn.image_batch(2, seed=1)
+    assert torch.equal(x1, x2) and float(x1.min()) >= 0 and float(x1.max()) < 1
+
+
+def test_net_plan_extraction():
+    m = build_flow(syn.CIFAR10_SMALL, 2)
+    blocks = imblocks(m)
+    e0 = _hip.net_entries(blocks[0].nnet_x)
+    e1 = _hip.net_entries(blocks[1].nnet_x)
+    kinds0 = [k for k, _ in e0]
+    kinds1 = [k for k, _ in e1]
+    assert kinds0 == [_hip.INF_LAYER_CONV, _hip.INF_ACT_SWISH, _hip.INF_LAYER_CONV, _hip.INF_ACT_SWISH,
+                      _hip.INF_LAYER_CONV]
+    assert kinds1 == [_hip.INF_ACT_SWISH] + kinds0          # preact block
+    assert _hip.net_entries(torch.nn.Sequential(torch.nn.Conv2d(3, 3, 3))) is None
+
+
+def test_product_path_refuses_cpu_tensors():
+    m = build_flow(syn.TOY, 4).eval()
+    m.load_state_dict(syn.make_state_dict(syn.TOY, 0))
+    with pytest.raises(_hip.HipError):
+        m(torch.zeros(4, 2), torch.zeros(4, 1))
