@@ -1,0 +1,183 @@
+#!/usr/bin/env python
+"""Throughput of the implicit-flow density-evaluation hot path on MI355X.
+
+Workload (BASELINE.json metric, config C3/C4): CIFAR10 3x32x32 implicit flow of run_cifar10.sh
+(3 scales x 2 imBlocks, idim 512, swish, kernels 3-1-3, coeff 0.9, preact, actnorm, logit init),
+model.eval(): per imBlock a Broyden root solve + two power-series Hutchinson log-dets with
+20 + Poisson(2) terms, then bits/dim.  One step = one batch of `--batch` images per GPU through
+the whole model; inputs are resident in HBM before the timed region.  Weights: deterministic
+random init of that architecture (lib/synthetic.py); data: synthetic dequantised images.
+Probes: device RNG by default (`--probes reference` replays the reference's CPU RNG stream).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU)
+
+Prints one JSON line on rank 0 (metric, value = samples/s over all ranks, roofline of the
+dominant kernel measured live with HIP events, cpu_baseline = the oracle on the host cores).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, 'implicit-normalizing-flows_amd')
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from lib import _hip, distributed as dd, synthetic as syn  # noqa: E402
+from lib.configs import build_flow, imblocks  # noqa: E402
+from lib.density import image_logpx  # noqa: E402
+from lib.layers import set_probe_mode  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=64, help='images per GPU')
+    ap.add_argument('--config', default='cifar10', choices=['cifar10', 'cifar10_small', 'celebahq256'])
+    ap.add_argument('--probes', default='device', choices=['device', 'reference'])
+    ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
+    ap.add_argument('--cpu-batch', type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(arch, sd, model, device, nimg):
+    """Oracle (CPU restatement, torch fp32, autograd VJPs) on a bounded sample; also the GPU path on
+    the same sample with the reference RNG replay -> |bpd_gpu - bpd_oracle|."""
+    from oracle import inflow_oracle as orc
+    cores = max(1, min(int(os.environ.get('OMP_NUM_THREADS', '16')), os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    x = syn.image_batch(nimg, arch['input_size'], arch['nvals'], seed=777)
+    flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
+    np.random.seed(11)
+    torch.manual_seed(11)
+    t0 = time.perf_counter()
+    ref_bpd, _, _ = orc.image_bits_per_dim(flow, x, arch['nvals'])
+    dt = time.perf_counter() - t0
+    set_probe_mode('reference')
+    np.random.seed(11)
+    torch.manual_seed(11)
+    gpu_bpd, _, _ = image_logpx(model, x.to(device), arch['nvals'])
+    torch.cuda.synchronize()
+    set_probe_mode('device')
+    return ({'value': nimg / dt, 'unit': 'samples/s', 'cores': cores, 'kind': 'port',
+             'sample': '%d CIFAR-shaped images through the full %s model (oracle/inflow_oracle.py, torch fp32 '
+                       'CPU, %d threads), %.1f s' % (nimg, 'run_cifar10.sh', cores, dt)},
+            abs(float(gpu_bpd) - float(ref_bpd)), float(ref_bpd))
+
+
+def main():
+    args = parse()
+    rank, world = dd.init_from_env()
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+    arch = syn.CONFIGS[args.config]
+    B = args.batch
+    sd = syn.make_state_dict(arch, 0, power_iters=30 if args.config != 'celebahq256' else 5)
+    model = build_flow(arch, B)
+    model.load_state_dict(sd, strict=True)
+    model = model.to(device).eval()
+    nsteps = args.warmup + args.steps
+    xs = torch.stack([syn.image_batch(B, arch['input_size'], arch['nvals'], seed=1000 * rank + i)
+                      for i in range(min(nsteps, 4))]).to(device)
+    ndim = int(np.prod(arch['input_size']))
+    set_probe_mode(args.probes, seed=12345 + rank)
+    np.random.seed(0)
+    torch.manual_seed(0)
+
+    def step(i):
+        _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
+        s, n = dd.global_logpx_sum(logpx)      # the one collective per batch
+        return dd.bits_per_dim(s, n, ndim)
+
+    for i in range(args.warmup):
+        step(i)
+    dd.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    bpd = None
+    for i in range(args.steps):
+        bpd = step(args.warmup + i)
+    torch.cuda.synchronize()
+    dd.barrier()
+    elapsed = dd.max_over_ranks(time.perf_counter() - t0, device)
+    value = world * B * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- live per-kernel timing (one extra step, outside the timed region) ----
+    steps_info = [b.last_broyden['nstep'] for b in imblocks(model)]
+    _hip.profile_begin(100000)
+    t1 = time.perf_counter()
+    step(0)
+    torch.cuda.synchronize()
+    prof_wall = time.perf_counter() - t1
+    stats = _hip.profile_end()
+    nps = [getattr(b, 'last_n_power_series', None) for b in imblocks(model)]
+    gemms = [s for s in stats if s['tag'] >= 1000]
+    dom = max(gemms, key=lambda s: s['total_ms'])
+    avg_ms = dom['total_ms'] / dom['launches']
+    achieved = dom['flops'] / dom['launches'] / (avg_ms * 1e-3) / 1e12
+    total_gemm_flops = sum(s['flops'] for s in gemms)
+    total_kernel_ms = sum(s['total_ms'] for s in stats)
+    traffic = None
+    pmc_path = os.path.join(REPO, 'profiles', 'pmc_dominant_kernel.json')
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get('tag') == dom['tag'] and pmc.get('batch') == B:
+                traffic = pmc.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+
+    out = {
+        'metric': 'samples/sec (whole node) + bits/dim delta vs ref, CIFAR10 density eval',
+        'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
+                % 'x'.join(map(str, arch['input_size'])),
+        'config': {'workload': '%s implicit flow density eval (run_cifar10.sh arch%s), batch %d per GPU'
+                               % (args.config, '' if args.config == 'cifar10' else ' variant', B),
+                   'global_batch': B * world, 'per_gpu_batch': B, 'parallelism': 'dp%d' % world,
+                   'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps},
+        'bits_per_dim': round(bpd, 6),
+        'roofline': {'bound': 'mfma', 'kernel': _hip.tag_name(dom['tag']), 'achieved': round(achieved, 2),
+                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
+                     'flops_per_launch': dom['flops'] / dom['launches']},
+        'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),
+                 'gemm_flop_rate_tflops': round(total_gemm_flops / (prof_wall * 1e12), 2),
+                 'kernel_busy_frac': round(total_kernel_ms / (prof_wall * 1e3), 3),
+                 'kernels': sorted([{'kernel': _hip.tag_name(s['tag']), 'launches': s['launches'],
+                                     'ms': round(s['total_ms'], 3),
+                                     'tflops': round(s['flops'] / (s['total_ms'] * 1e9), 2) if s['flops'] else None,
+                                     'gbs': round(s['bytes'] / (s['total_ms'] * 1e6), 1)}
+                                    for s in stats], key=lambda r: -r['ms'])[:8]},
+        'cpu_baseline': None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline and args.config != 'celebahq256':
+        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch)
+        out['cpu_baseline'] = cb
+        out['bpd_delta_vs_oracle'] = delta
+        out['speedup_vs_cpu_baseline'] = round(value / cb['value'], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

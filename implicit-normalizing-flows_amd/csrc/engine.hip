@@ -23,6 +23,25 @@
 namespace inf {
 static thread_local int g_last_hip = 0;
 void set_hip_error(hipError_t e) { g_last_hip = (int)e; }
+
+// ---- opt-in launch timing -------------------------------------------------------------------
+struct ProfSlot {
+  hipEvent_t a, b;
+  int tag;
+  double flops, bytes;
+};
+static std::vector<ProfSlot> g_prof;
+static size_t g_prof_used = 0;
+static bool g_prof_on = false;
+bool prof_enabled() { return g_prof_on && g_prof_used < g_prof.size(); }
+void prof_begin_launch(hipStream_t s) { (void)hipEventRecord(g_prof[g_prof_used].a, s); }
+void prof_end_launch(hipStream_t s, int tag, double flops, double bytes) {
+  ProfSlot& p = g_prof[g_prof_used++];
+  (void)hipEventRecord(p.b, s);
+  p.tag = tag;
+  p.flops = flops;
+  p.bytes = bytes;
+}
 }  // namespace inf
 
 using namespace inf;
@@ -786,6 +805,53 @@ int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, co
   ba.m = (nstep - 1) % T;
   ba.ncols = std::min(nstep, T);
   return launch_broyden_update(ba, (hipStream_t)stream);
+}
+
+// ---- launch timing --------------------------------------------------------------------------
+int inf_profile_begin(int max_launches) {
+  if (max_launches <= 0) return INF_ERR_INVALID;
+  for (auto& p : g_prof) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  g_prof.assign((size_t)max_launches, ProfSlot{});
+  for (auto& p : g_prof) {
+    INF_HIP(hipEventCreate(&p.a));
+    INF_HIP(hipEventCreate(&p.b));
+  }
+  g_prof_used = 0;
+  g_prof_on = true;
+  return INF_OK;
+}
+
+int inf_profile_end(InfKernelStat* out, int max_out, int* n_out) {
+  g_prof_on = false;
+  std::vector<InfKernelStat> agg;
+  for (size_t i = 0; i < g_prof_used; ++i) {
+    ProfSlot& p = g_prof[i];
+    INF_HIP(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    INF_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    InfKernelStat* st = nullptr;
+    for (auto& s : agg)
+      if (s.tag == p.tag) st = &s;
+    if (!st) {
+      InfKernelStat z;
+      memset(&z, 0, sizeof(z));
+      z.tag = p.tag;
+      agg.push_back(z);
+      st = &agg.back();
+    }
+    st->launches += 1;
+    st->total_ms += ms;
+    st->flops += p.flops;
+    st->bytes += p.bytes;
+  }
+  const int n = (int)std::min<size_t>(agg.size(), (size_t)std::max(max_out, 0));
+  for (int i = 0; i < n; ++i) out[i] = agg[i];
+  if (n_out) *n_out = (int)agg.size();
+  g_prof_used = 0;
+  return INF_OK;
 }
 
 // ---- flow glue ------------------------------------------------------------------------------

@@ -252,9 +252,19 @@ static int run(const GemmArgs& g, hipStream_t s) {
   const long nb = (long)nMt * nNt;
   if (nb <= 0) return INF_OK;
   if (nb > 0x7fffffffL) return INF_ERR_INVALID;
+  const bool prof = prof_enabled();
+  if (prof) prof_begin_launch(s);
   hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, TN, BLOAD, EPI, VEC>), dim3((unsigned)nb), dim3(WM * WN * 64), 0,
                      s, g);
   INF_CHECK_LAUNCH();
+  if (prof) {
+    // tag = instantiation id; algorithmic work: 2*M*N*K flops, bytes = A + B operand + output (+ deriv)
+    const int tag = ((WM * 10 + WN) * 100 + TM * 10 + TN) * 1000 + BLOAD * 100 + EPI * 10 + (VEC ? 1 : 0);
+    const double flops = 2.0 * g.M * (double)g.N * g.Ktot;
+    const bool dio = EPI == EP_MUL_DERIV || ((EPI >= EP_ACT_SWISH) && g.deriv_out);
+    const double bytes = 4.0 * ((double)g.M * g.Ktot + (double)g.Ktot * g.N + (double)g.M * g.N * (1 + (dio ? 1 : 0)));
+    prof_end_launch(s, tag, flops, bytes);
+  }
   return INF_OK;
 }
 

@@ -109,4 +109,13 @@ int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, 
 int launch_series_combine(const double* partials, const float* coeff_dev, int n_terms, int batch, int nchunk,
                           float* out, hipStream_t s);
 
+// ------------------------------------------------------------------------------------------
+// opt-in launch timing (inf_profile_begin/end): hipEvents around every engine kernel launch,
+// tagged with the kernel instantiation and its algorithmic FLOPs / bytes.  Off by default; a
+// debug/measurement facility, not re-entrant.
+// ------------------------------------------------------------------------------------------
+bool prof_enabled();
+void prof_begin_launch(hipStream_t s);
+void prof_end_launch(hipStream_t s, int tag, double flops, double bytes);
+
 }  // namespace inf

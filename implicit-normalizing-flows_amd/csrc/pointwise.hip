@@ -80,11 +80,18 @@ __global__ __launch_bounds__(256) void conv_out_kernel(OutArgs a) {
 int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
   const int per = a.C * a.H * a.W;
   dim3 grid(out_nchunk(per), batch);
+  const bool prof = prof_enabled();
+  if (prof) prof_begin_launch(s);
   if (a.ks == 1)
     hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(conv_out_kernel<3>, grid, dim3(256), 0, s, a);
   INF_CHECK_LAUNCH();
+  if (prof) {
+    // bytes: the Y rows read (9 taps or 1) + ~3 per-element vectors in/out
+    const double bytes = 4.0 * (double)batch * per * (a.ks == 3 ? 9 : 1) + 12.0 * (double)batch * per;
+    prof_end_launch(s, 900 + a.mode * 10 + a.ks, 0.0, bytes);
+  }
   return INF_OK;
 }
 

@@ -41,6 +41,11 @@ class BroydenStats(ctypes.Structure):
                 'threshold': threshold, 'fixed_point_iters': self.fixed_point_iters}
 
 
+class KernelStat(ctypes.Structure):
+    _fields_ = [('tag', ctypes.c_int), ('launches', ctypes.c_int), ('total_ms', ctypes.c_double),
+                ('flops', ctypes.c_double), ('bytes', ctypes.c_double)]
+
+
 class HipError(RuntimeError):
     pass
 
@@ -75,6 +80,8 @@ _SIGS = {
     'inf_actnorm_forward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     'inf_squeeze2': (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     'inf_normal_logprob': (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
+    'inf_profile_begin': (ctypes.c_int, [ctypes.c_int]),
+    'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
 }
 EXPORTS = tuple(_SIGS)
@@ -249,3 +256,29 @@ def native_net(module, shape, device):
     net = NativeNet(entries, shape, device)
     cache[key] = net
     return net
+
+
+def profile_begin(max_launches=200000):
+    check(load().inf_profile_begin(int(max_launches)), 'inf_profile_begin')
+
+
+def profile_end():
+    """Per-instantiation launch statistics since profile_begin (synchronises)."""
+    arr = (KernelStat * 256)()
+    n = ctypes.c_int()
+    check(load().inf_profile_end(arr, 256, ctypes.byref(n)), 'inf_profile_end')
+    return [dict(tag=arr[i].tag, launches=arr[i].launches, total_ms=arr[i].total_ms, flops=arr[i].flops,
+                 bytes=arr[i].bytes) for i in range(min(n.value, 256))]
+
+
+def tag_name(tag):
+    """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
+    if tag < 1000:
+        modes = {0: 'PLAIN', 1: 'EMBED', 2: 'RESID', 3: 'RECOMP', 4: 'VJP'}
+        return 'conv_out_kernel<%d> mode %s' % (tag % 10, modes.get((tag - 900) // 10, '?'))
+    vec, epi, bload = tag % 10, (tag // 10) % 10, (tag // 100) % 10
+    cfg = tag // 1000
+    wm, wn, tm, tn = cfg // 1000, (cfg // 100) % 10, (cfg // 10) % 10, cfg % 10
+    epis = {0: 'STORE', 1: 'BIAS', 3: 'MUL_DERIV', 4: 'BIAS_PRIMAL', 5: 'ACT_SWISH', 6: 'ACT_SIN', 7: 'ACT_NONE'}
+    return 'gemm_f32_kernel<%d,%d,%d,%d,%s,%s,%s>' % (wm, wn, tm, tn, ['DIRECT', 'IM2COL3'][bload],
+                                                        epis.get(epi, str(epi)), 'true' if vec else 'false')

@@ -1,0 +1,62 @@
+"""Data-parallel density evaluation: one process per GPU (torchrun), contiguous batch shards, and
+one all-reduce of [sum log p(x), N] in fp64 per evaluated batch (RCCL over xGMI with the nccl
+backend; gloo on CPU).  Replaces the reference's nn.DataParallel (train_img.py:203-204), which
+re-broadcasts every parameter on every forward and gathers outputs to device 0.
+"""
+import math
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def init_from_env(backend=None):
+    """Initialise the default group from torchrun's env (RANK/WORLD_SIZE/MASTER_*); no-op for 1 rank."""
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    if ws <= 1 or (dist.is_available() and dist.is_initialized()):
+        return world()
+    if backend is None:
+        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    if backend == 'nccl':
+        torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
+    dist.init_process_group(backend=backend)
+    return world()
+
+
+def shard(n_total, rank, world_size):
+    """Contiguous [lo, hi) rows of rank `rank` (sizes differ by at most one)."""
+    base, rem = divmod(n_total, world_size)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def global_logpx_sum(logpx_local):
+    """All-reduce [sum log p(x), N] (fp64) over the default group; returns python floats."""
+    t = torch.stack([logpx_local.double().sum(), torch.tensor(float(logpx_local.numel()), dtype=torch.float64,
+                                                                  device=logpx_local.device)])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t[0]), float(t[1])
+
+
+def bits_per_dim(sum_logpx, count, ndim):
+    return -(sum_logpx / count) / ndim / math.log(2)
+
+
+def max_over_ranks(value, device):
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()

@@ -138,6 +138,17 @@ int inf_normal_logprob(const float* z, float* out, int batch, int per_sample, vo
  * draws probes on the host, implicit_block.py:297-298). */
 int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* stream);
 
+/* ---- measurement: opt-in per-launch timing with HIP events (not re-entrant; off by default) ---- */
+typedef struct InfKernelStat {
+  int tag;          /* kernel instantiation id ("Kernel tags") */
+  int launches;
+  double total_ms;  /* sum of event-measured launch durations */
+  double flops;     /* algorithmic FLOPs of those launches */
+  double bytes;     /* algorithmic bytes of those launches */
+} InfKernelStat;
+int inf_profile_begin(int max_launches);
+int inf_profile_end(InfKernelStat* out, int max_out, int* n_out);
+
 #ifdef __cplusplus
 }
 #endif
