@@ -11,6 +11,7 @@
 //   inf_logdet_neumann    <- neumann_logdet_estimator                                    (:429-438)
 //   inf_logdet_exact      <- brute-force batch_jacobian + torch.logdet                   (:249-260)
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -85,6 +86,10 @@ struct InfNet {
   double* scratch = nullptr;
   size_t scratch_doubles = 0;
   int device = 0;
+  // fused 3-1-3 path (fused313.hip): fragment-major operands for forward (f) and VJP (b)
+  bool fused = false;
+  int fhid = 0, K1pad = 0, M3 = 0, M3pad = 0;
+  float *F1f = nullptr, *F1b = nullptr, *F2f = nullptr, *F2b = nullptr, *F3f = nullptr, *F3b = nullptr;
 };
 
 namespace {
@@ -193,8 +198,50 @@ void set_out(const InfNet* n, GemmArgs& g, float* out, int out_rows) {
 
 // Forward chain.  mode = OM_* for the output stage, or -1 for "save derivatives only" (log-det prep:
 // the last layer is skipped, D[l] = act'(a_l) are kept).  x is in internal layout.
+Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool vjp) {
+  Net313Args f;
+  memset(&f, 0, sizeof(f));
+  f.in = in;
+  f.pre_beta = vjp ? nullptr : n->pre_beta;
+  f.A1 = vjp ? n->F1b : n->F1f;
+  f.K1pad = n->K1pad;
+  f.A2 = vjp ? n->F2b : n->F2f;
+  f.A3 = vjp ? n->F3b : n->F3f;
+  f.M3 = n->M3;
+  f.M3pad = n->M3pad;
+  f.b1 = n->L[0].b;
+  f.beta1 = n->L[0].act_beta;
+  f.b2 = n->L[1].b;
+  f.beta2 = n->L[1].act_beta;
+  f.d1 = bf.D[0];
+  f.d2 = bf.D[1];
+  f.Y = bf.Y;
+  f.B = B;
+  f.C = n->C;
+  f.H = n->H;
+  f.W = n->W;
+  f.seg = n->W < 64 ? n->W : 64;
+  return f;
+}
+
 int run_forward(InfNet* n, const float* x, int B, Bufs& bf, int mode, const OutArgs* oa, hipStream_t s) {
   const int L = (int)n->L.size();
+  if (n->fused) {
+    Net313Args f = net313_args(n, x, B, bf, false);
+    INF_TRY(launch_net313(f, n->fhid, mode < 0 ? MODE_SAVE : MODE_EVAL, s));
+    if (mode < 0) return INF_OK;
+    OutArgs a = *oa;
+    a.Y = bf.Y;
+    a.y_sample = (long)n->M3 * n->P;
+    a.C = n->C;
+    a.H = n->H;
+    a.W = n->W;
+    a.ks = 3;
+    a.mode = mode;
+    a.bias = n->L[2].b;
+    a.pre_beta = nullptr;
+    return launch_conv_out(a, B, s);
+  }
   const float* cur = x;
   int cur_ch = n->C;
   for (int l = 0; l < L - 1; ++l) {
@@ -236,6 +283,26 @@ int run_forward(InfNet* n, const float* x, int B, Bufs& bf, int mode, const OutA
 int run_vjp(InfNet* n, const float* v, float* vout, const float* xin, const float* eps, double* partial, int B,
             Bufs& bf, hipStream_t s) {
   const int L = (int)n->L.size();
+  if (n->fused) {
+    Net313Args f = net313_args(n, v, B, bf, true);
+    INF_TRY(launch_net313(f, n->fhid, MODE_VJP, s));
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Y = bf.Y;
+    a.y_sample = (long)n->M3 * n->P;
+    a.C = n->C;
+    a.H = n->H;
+    a.W = n->W;
+    a.ks = 3;
+    a.mode = OM_VJP;
+    a.in0 = eps;
+    a.in1 = xin;
+    a.out0 = vout;
+    a.pre_beta = n->pre_beta;
+    a.partial = partial;
+    a.nchunk = out_nchunk(n->d);
+    return launch_conv_out(a, B, s);
+  }
   const float* cur = v;
   int cur_ch = n->C;
   for (int l = L - 1; l >= 1; --l) {
@@ -550,6 +617,22 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     if (first) n->rows_max = std::max(n->rows_max, w.g.M);
   }
   if (L == 1) n->hidden_max = std::max(n->hidden_max, 1);
+  // fused 3-1-3 conv net (run_cifar10.sh nets): 3x3 C->H, swish, 1x1 H->H, swish, 3x3 H->C
+  {
+    const char* off = getenv("INFLOW_NO_FUSED");
+    const bool shape_ok = !n->fc && L == 3 && n->L[0].ks == 3 && n->L[1].ks == 1 && n->L[2].ks == 3 &&
+                          n->L[0].act == ACT_SWISH && n->L[1].act == ACT_SWISH &&
+                          n->L[0].cout == n->L[1].cin && n->L[1].cin == n->L[1].cout && n->L[1].cout == n->L[2].cin;
+    if (shape_ok && !(off && off[0] == '1') && net313_supported(n->L[1].cout, n->C, n->H, n->W)) {
+      n->fused = true;
+      n->fhid = n->L[1].cout;
+      n->K1pad = round_up(9 * n->C, 16);
+      n->M3 = 9 * n->C;
+      n->M3pad = round_up(9 * n->C, 32);
+      floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
+      n->rows_max = std::max(n->rows_max, n->M3);
+    }
+  }
   // sigma scratch: one partial per 256 output elements of the largest conv
   size_t sc = 64;
   for (auto& w : n->L) sc = std::max(sc, (size_t)w.cout * (n->fc ? 1 : n->P) / 256 + 64);
@@ -569,6 +652,15 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     }
     w.factor = p;
     p += 64;
+  }
+  if (n->fused) {
+    float** bufs[] = {&n->F1f, &n->F1b, &n->F2f, &n->F2b, &n->F3f, &n->F3b};
+    const size_t sz[] = {(size_t)n->fhid * n->K1pad, (size_t)n->fhid * n->K1pad, (size_t)n->fhid * n->fhid,
+                         (size_t)n->fhid * n->fhid, (size_t)n->M3pad * n->fhid, (size_t)n->M3pad * n->fhid};
+    for (int i = 0; i < 6; ++i) {
+      *bufs[i] = p;
+      p += sz[i] + 64;
+    }
   }
   *out = n;
   return INF_OK;
@@ -591,6 +683,16 @@ int inf_net_refresh(InfNet* n, void* stream) {
                          reinterpret_cast<float*>(n->scratch), s));
     INF_TRY(launch_pack(w.W, w.factor, w.f.A, w.cout, w.cin, w.ks, w.f.Mpad, w.f.Kpad, w.f.pack, s));
     INF_TRY(launch_pack(w.W, w.factor, w.g.A, w.cout, w.cin, w.ks, w.g.Mpad, w.g.Kpad, w.g.pack, s));
+  }
+  if (n->fused) {
+    const WLayer &l0 = n->L[0], &l1 = n->L[1], &l2 = n->L[2];
+    const int H = n->fhid;
+    INF_TRY(launch_pack(l0.W, l0.factor, n->F1f, l0.cout, l0.cin, 3, H, n->K1pad, PK_IM2COL_FWD, s, 1));
+    INF_TRY(launch_pack(l2.W, l2.factor, n->F1b, l2.cout, l2.cin, 3, H, n->K1pad, PK_IM2COL_BWD, s, 1));
+    INF_TRY(launch_pack(l1.W, l1.factor, n->F2f, H, H, 1, H, H, PK_ROWMAJOR, s, 1));
+    INF_TRY(launch_pack(l1.W, l1.factor, n->F2b, H, H, 1, H, H, PK_TRANSPOSE, s, 1));
+    INF_TRY(launch_pack(l2.W, l2.factor, n->F3f, l2.cout, l2.cin, 3, n->M3pad, H, PK_TAPS_FWD, s, 1));
+    INF_TRY(launch_pack(l0.W, l0.factor, n->F3b, l0.cout, l0.cin, 3, n->M3pad, H, PK_TAPS_BWD, s, 1));
   }
   return INF_OK;
 }

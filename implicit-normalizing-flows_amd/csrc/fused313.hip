@@ -1,0 +1,366 @@
+// Fused "3-1-3" conv-net kernel: the whole residual branch of a run_cifar10.sh imBlock,
+//   [preact swish] -> conv3x3 C->HID -> swish -> conv1x1 HID->HID -> swish -> conv3x3 HID->C
+// (implicit_flow.py:362-399), for one tile of 64 pixels of one image per workgroup, in three MFMA
+// phases that keep the HID x 64 activation tile resident in LDS:
+//
+//   phase A  t = W_A . im2col3(in)          K = 9C  (in = x or the VJP vector v; halo tile in LDS)
+//   phase B  t = W_B . t                    K = HID (t read from LDS, written back to LDS)
+//   phase C  Y = W_C . t                    K = HID, M = 9C packed taps -> HBM; conv_out sums the taps
+//
+// Modes (what the per-phase epilogues do):
+//   MODE_EVAL  forward value  : A: swish(a + b1)        B: swish(a + b2)         C: taps of W3
+//   MODE_SAVE  forward, saving: A: d1 = swish'(a + b1)  B: d2 = swish'(a + b2)   (no phase C; the
+//              log-det estimator only needs the activation derivatives, implicit_block.py:318-319)
+//   MODE_VJP   v^T J          : A: (W3^T-flipped . v) * d2   B: (W2^T . t) * d1   C: taps of W1^T
+// so one VJP of the series costs one launch that reads d1, d2 (the minimal HBM traffic) instead of
+// three GEMM launches that round-trip two HID-channel tensors through HBM.
+//
+// Weights are packed "fragment-major" (pack mode PK_*, frag = 1): for row block rb (32 rows) and K
+// tile kt (16) the 64 lanes' A fragments (A[32rb + (l&31)][16kt + 8(l>>5) + kk], kk < 8) are 2 KB
+// contiguous, so each wave streams its A operand straight from L2 into registers with two
+// dwordx4 loads per row block (no LDS for A).  B fragments come from LDS: one ds_read2_b32 per
+// MFMA k-step (32 lanes read 32 consecutive floats: conflict-free).
+// 8 waves x (TM*32 rows) cover HID = 256*TM rows; each wave owns 2 x 32 pixel columns.
+#include "kernels.h"
+
+namespace inf {
+
+constexpr int F_BN = 64;          // pixels per tile
+constexpr int F_LDS_FLOATS = 40960;   // 160 KiB
+
+__device__ __forceinline__ void load_frag8(const float* base, float* o) {
+  const f32x4 v0 = *reinterpret_cast<const f32x4*>(base);
+  const f32x4 v1 = *reinterpret_cast<const f32x4*>(base + 4);
+  o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = v0.w;
+  o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = v1.w;
+}
+
+// fragment-major offset of (row block rb, k tile kt) for a matrix with nkt K tiles
+__device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
+  return (((long)rb * nkt + kt) * 64 + lane) * 8;
+}
+
+template <int TM, int MODE>
+__global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
+  constexpr int HID = 8 * 32 * TM;
+  __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
+  float* t = smem;                                  // [HID][64] activation tile
+  int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
+  float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile (+1 zero slot)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int P = a.H * a.W;
+  const int tiles_per_img = P / F_BN;
+  const int img = blockIdx.x / tiles_per_img, tile = blockIdx.x - img * tiles_per_img;
+  const int p0 = tile * F_BN;
+  // tile geometry: `rows` image rows of `seg` pixels (seg = min(W, 64))
+  const int seg = a.seg, rows = F_BN / seg;
+  const int y0 = p0 / a.W, x0 = p0 - y0 * a.W;
+  const int RH = rows + 2, CW = seg + 2;
+  const int vhn = a.C * RH * CW;
+
+  // ---- stage the input halo tile (zero padded; forward applies the preact swish) ----
+  const float* in = a.in + (long)img * a.C * P;
+  const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+  for (int i = tid; i <= vhn; i += 512) {
+    float v = 0.f;
+    if (i < vhn) {
+      const int c = i / (RH * CW), rr = i - c * RH * CW;
+      const int hy = rr / CW, hx = rr - hy * CW;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+        v = in[(long)c * P + yy * a.W + xx];
+        if (a.pre_beta) v = swish_f(v, pre_sp);
+      }
+    }
+    vh[i] = v;
+  }
+  for (int k = tid; k < a.K1pad; k += 512) {
+    int o = vhn;                                    // zero slot for the K padding
+    if (k < 9 * a.C) {
+      const int c = k / 9, tt = k - c * 9;
+      o = c * RH * CW + (tt / 3) * CW + (tt % 3);
+    }
+    koff[k] = o;
+  }
+  // pixel offsets of this lane's two columns inside the halo tile, and in the image
+  int pix[2], gp[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int n = b * 32 + li;
+    const int py = n / seg, px = n - py * seg;
+    pix[b] = py * CW + px;
+    gp[b] = (y0 + py) * a.W + x0 + px;
+  }
+  const long plane = (long)img * HID * P;           // sample offset of HID-channel tensors
+  const int rbw = wid * TM;                          // this wave's first 32-row block
+  auto row_of = [&](int m, int r) { return (rbw + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh; };
+  // HID-channel HBM tensors: one base pointer per (row block, column); element r of the MFMA tile
+  // is at base[roff(r)] with the wave-uniform row offset roff(r) = ((r&3) + 8(r>>2)) * P.
+  auto hid_base = [&](float* base, int m, int b) {
+    return base + plane + (long)((rbw + m) * 32 + 4 * lh) * P + gp[b];
+  };
+  auto roff = [&](int r) { return ((r & 3) + 8 * (r >> 2)) * P; };
+
+  // VJP: prefetch the phase-A multiplier d2 (retired by the phase-A loop's waits)
+  float dmul[TM][2][16];
+  if constexpr (MODE == MODE_VJP) {
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+          const float* src = hid_base(a.d2, m, b);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dmul[m][b][r] = src[roff(r)];
+      }
+  }
+  __syncthreads();
+
+  f32x16 acc[TM][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[m][b][r] = 0.f;
+  };
+
+  // ---------------------------------------------------------------- phase A: K = 9C (im2col)
+  zero_acc();
+  {
+    const int nkt = a.K1pad / 16;
+    float af[2][TM][8];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, 0, nkt, lane), af[0][m]);
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, kt + 1, nkt, lane), af[cur ^ 1][m]);
+      }
+      int ko[8];
+      {
+        const int* kp = koff + kt * 16 + lh * 8;
+        const int4 k0 = *reinterpret_cast<const int4*>(kp);
+        const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
+        ko[0] = k0.x; ko[1] = k0.y; ko[2] = k0.z; ko[3] = k0.w;
+        ko[4] = k1.x; ko[5] = k1.y; ko[6] = k1.z; ko[7] = k1.w;
+      }
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const float b0 = vh[ko[kk] + pix[0]], b1 = vh[ko[kk] + pix[1]];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b0, acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b1, acc[m][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue A -> t (LDS); SAVE: d1 -> HBM
+  {
+    const float sp1 = (MODE != MODE_VJP) ? softplus_f(*a.beta1) : 0.f;
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* dst = (MODE == MODE_SAVE) ? hid_base(a.d1, m, b) : nullptr;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = row_of(m, r);
+          float v;
+          if constexpr (MODE == MODE_VJP) {
+            v = acc[m][b][r] * dmul[m][b][r];
+          } else {
+            const float z = acc[m][b][r] + a.b1[o];
+            v = swish_f(z, sp1);
+            if constexpr (MODE == MODE_SAVE) dst[roff(r)] = swish_d(z, sp1);
+          }
+          t[o * F_BN + b * 32 + li] = v;
+        }
+      }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- phase B: K = HID (from LDS)
+  zero_acc();
+  {
+    constexpr int nkt = HID / 16;
+    float af[2][TM][8];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, 0, nkt, lane), af[0][m]);
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, kt + 1, nkt, lane), af[cur ^ 1][m]);
+      }
+      const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const float b0 = tb[kk * F_BN], b1 = tb[kk * F_BN + 32];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b0, acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b1, acc[m][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if constexpr (MODE == MODE_SAVE) {
+    const float sp2 = softplus_f(*a.beta2);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* dst = hid_base(a.d2, m, b);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[roff(r)] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
+      }
+    return;
+  } else {
+    // epilogue B -> t (after every wave finished reading t).  VJP: the multiplier d1 is loaded here,
+    // not prefetched across the phase-B loop (64 more live registers there would spill).
+    if constexpr (MODE == MODE_VJP) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+        {
+          const float* src = hid_base(a.d1, m, b);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dmul[m][b][r] = src[roff(r)];
+        }
+    }
+    const float sp2 = (MODE == MODE_EVAL) ? softplus_f(*a.beta2) : 0.f;
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = row_of(m, r);
+          if constexpr (MODE == MODE_VJP) acc[m][b][r] = acc[m][b][r] * dmul[m][b][r];
+          else acc[m][b][r] = swish_f(acc[m][b][r] + a.b2[o], sp2);
+        }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
+    __syncthreads();
+
+    // -------------------------------------------------------------- phase C: taps, K = HID
+    // tasks = (32-row block of the M3pad tap rows) x (32-pixel column); split K when there are
+    // fewer tasks than waves, partial tiles reduced through LDS.
+    const int nrb = a.M3pad / 32;
+    const int ntask = nrb * 2;
+    int ksplit = 1;
+    while (ntask * ksplit * 2 <= 8 && ksplit < 8) ksplit *= 2;
+    constexpr int nkt = HID / 16;
+    const int kts = nkt / ksplit;
+    const int njobs = ntask * ksplit;
+    float* part = smem;          // reuse t after the barrier below (ksplit > 1 only)
+    f32x16 cacc[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int job = wid + 8 * jj;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
+      if (job >= njobs) continue;
+      const int task = job / ksplit, ks = job - task * ksplit;
+      const int rb = task >> 1, b = task & 1;
+      for (int kt = ks * kts; kt < (ks + 1) * kts; ++kt) {
+        float af[8];
+        load_frag8(a.A3 + frag_off(rb, kt, nkt, lane), af);
+        const float* tb = t + (kt * 16 + lh * 8) * F_BN + b * 32 + li;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          cacc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk], tb[kk * F_BN], cacc[jj], 0, 0, 0);
+      }
+    }
+    float* Y = a.Y + (long)img * a.M3 * P;
+    if (ksplit == 1) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int job = wid + 8 * jj;
+        if (job >= njobs) continue;
+        const int rb = job >> 1, b = job & 1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M3) Y[(long)row * P + gp[b]] = cacc[jj][r];
+        }
+      }
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int job = wid + 8 * jj;
+        if (job >= njobs) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[(job * 16 + r) * 64 + lane] = cacc[jj][r];
+      }
+      __syncthreads();
+      // one wave per task sums its ksplit partials
+      for (int task = wid; task < ntask; task += 8) {
+        const int rb = task >> 1, b = task & 1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float s = 0.f;
+          for (int ks = 0; ks < ksplit; ++ks) s += part[((task * ksplit + ks) * 16 + r) * 64 + lane];
+          const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < a.M3) Y[(long)row * P + gp[b]] = s;
+        }
+      }
+    }
+  }
+}
+
+int net313_supported(int hid, int C, int H, int W) {
+  if (hid != 512 && hid != 256) return 0;
+  const int P = H * W;
+  const int seg = W < F_BN ? W : F_BN;
+  if (P % F_BN != 0 || F_BN % seg != 0 || (W > F_BN && W % F_BN != 0)) return 0;
+  const int rows = F_BN / seg;
+  const long k1pad = (9L * C + 15) / 16 * 16;
+  const long need = (long)hid * F_BN + k1pad + (long)C * (rows + 2) * (seg + 2) + 1;
+  if (need > F_LDS_FLOATS) return 0;
+  const long m3pad = (9L * C + 31) / 32 * 32;
+  if ((m3pad / 32) * 2 > 32) return 0;            // at most 4 phase-C jobs per wave
+  return 1;
+}
+
+int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s) {
+  if (!net313_supported(hid, a.C, a.H, a.W)) return INF_ERR_UNSUPPORTED;
+  const int P = a.H * a.W;
+  const unsigned nb = (unsigned)(a.B * (P / F_BN));
+  const bool prof = prof_enabled();
+  if (prof) prof_begin_launch(s);
+#define L313(TM_, MODE_) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, a)
+  if (hid == 512) {
+    if (mode == MODE_EVAL) L313(2, MODE_EVAL);
+    else if (mode == MODE_SAVE) L313(2, MODE_SAVE);
+    else L313(2, MODE_VJP);
+  } else {
+    if (mode == MODE_EVAL) L313(1, MODE_EVAL);
+    else if (mode == MODE_SAVE) L313(1, MODE_SAVE);
+    else L313(1, MODE_VJP);
+  }
+#undef L313
+  INF_CHECK_LAUNCH();
+  if (prof) {
+    const double npx = (double)a.B * P;
+    const double fA = 2.0 * hid * 9.0 * a.C, fB = 2.0 * hid * hid, fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a.C * hid;
+    const double bytes = 4.0 * npx * (a.C + (mode == MODE_SAVE ? 2.0 * hid : (mode == MODE_VJP ? 2.0 * hid : 0.0)) +
+                                      (mode == MODE_SAVE ? 0.0 : 9.0 * a.C));
+    prof_end_launch(s, 500 + mode, npx * (fA + fB + fC), bytes);
+  }
+  return INF_OK;
+}
+
+}  // namespace inf

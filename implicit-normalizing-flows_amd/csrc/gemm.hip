@@ -52,6 +52,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs g) {
 
   const float pre_sp = g.pre_beta ? softplus_f(*g.pre_beta) : 0.f;
 
+  // ---- epilogue geometry: C/D map of the 32x32 f32 MFMA is col = lane&31,
+  //      row = (r&3) + 8*(r>>2) + 4*(lane>>5); element (a, b, r) lives at out[obase[b] + m(a,r) * P] ----
+
   // ---- per-thread B-loader geometry (column ownership is fixed across K tiles) ----
   // VEC DIRECT: thread owns float4 column group c4 = tid % (BN/4), rows kr0 + i*(NT*4/BN)
   // scalar / IM2COL3: thread owns column j = tid % BN, rows kr0 + i*(NT/BN)
@@ -159,6 +162,37 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs g) {
     }
   };
 
+  const float act_sp = (EPI == EP_ACT_SWISH) ? softplus_f(*g.act_beta) : 0.f;
+  long obase[TN];
+  bool nok[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wn * TN * 32 + b * 32 + li;
+    nok[b] = n < g.N;
+    const int sb = nok[b] ? n / g.P : 0, p = nok[b] ? n - sb * g.P : 0;
+    obase[b] = (long)sb * g.o_sample + p;
+  }
+  const int mrow0 = m0 + wm * TM * 32 + 4 * lh;
+  auto mrow = [&](int a, int r) { return mrow0 + a * 32 + (r & 3) + 8 * (r >> 2); };
+  // Interior tiles (the common case) take a branch-free epilogue.  For EP_MUL_DERIV the multiplier
+  // tile is loaded here, before the K loop: the loop's own waits retire these loads, so the
+  // epilogue issues stores only (gfx950 counts stores in vmcnt; 64 loads + stores in flight would
+  // otherwise force a vmcnt(0) per element).
+  const bool interior = (m0 + BM <= g.M) && (n0 + BN <= g.N);
+  float dv[EPI == EP_MUL_DERIV ? TM : 1][EPI == EP_MUL_DERIV ? TN : 1][16];
+  if constexpr (EPI == EP_MUL_DERIV) {
+    if (interior) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const float* src = g.deriv_in + obase[b];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dv[a][b][r] = src[(long)mrow(a, r) * g.P];
+        }
+    }
+  }
+
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -202,30 +236,92 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs g) {
     }
   }
 
-  // ---- epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5) ----
-  const float act_sp = (EPI == EP_ACT_SWISH) ? softplus_f(*g.act_beta) : 0.f;
+  // ---- epilogue (geometry and EP_MUL_DERIV multipliers were set up before the K loop) ----
+  // Interior tiles (the common case) take a branch-free path: with per-element exec-masked stores
+  // the compiler cannot count vmcnt (gfx950 counts stores too) and waits vmcnt(0) per element.
+  if constexpr (EPI == EP_MUL_DERIV) {
+    if (interior) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          float* dst = g.out + obase[b];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[(long)mrow(a, r) * g.P] = acc[a][b][r] * dv[a][b][r];
+        }
+      return;
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow(a, r);
+          dv[a][b][r] = (nok[b] && m < g.M) ? g.deriv_in[obase[b] + (long)m * g.P] : 0.f;
+        }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow(a, r);
+          if (nok[b] && m < g.M) g.out[obase[b] + (long)m * g.P] = acc[a][b][r] * dv[a][b][r];
+        }
+    return;
+  }
+  if (interior) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow(a, r);
+          const long o = obase[b] + (long)m * g.P;
+          const float v = acc[a][b][r];
+          if constexpr (EPI == EP_STORE) {
+            g.out[o] = v;
+          } else if constexpr (EPI == EP_BIAS) {
+            g.out[o] = v + g.bias[m];
+          } else if constexpr (EPI == EP_BIAS_PRIMAL) {
+            g.out[o] = (n0 + wn * TN * 32 + b * 32 + li) < g.n_primal ? v + g.bias[m] : v;
+          } else {
+            const float z = v + g.bias[m];
+            if constexpr (EPI == EP_ACT_SWISH) {
+              if (g.deriv_out) g.deriv_out[o] = swish_d(z, act_sp);
+              if (g.write_out) g.out[o] = swish_f(z, act_sp);
+            } else if constexpr (EPI == EP_ACT_SIN) {
+              if (g.deriv_out) g.deriv_out[o] = sinact_d(z);
+              if (g.write_out) g.out[o] = sinact_f(z);
+            } else {
+              if (g.deriv_out) g.deriv_out[o] = 1.f;
+              if (g.write_out) g.out[o] = z;
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int n = n0 + wn * TN * 32 + b * 32 + li;
-    if (n >= g.N) continue;
-    const int sb = n / g.P, p = n - sb * g.P;
-    const long obase = (long)sb * g.o_sample + p;
+    if (!nok[b]) continue;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int m = mrow(a, r);
         if (m >= g.M) continue;
-        const long o = obase + (long)m * g.P;
-        float v = acc[a][b][r];
+        const long o = obase[b] + (long)m * g.P;
+        const float v = acc[a][b][r];
         if constexpr (EPI == EP_STORE) {
           g.out[o] = v;
         } else if constexpr (EPI == EP_BIAS) {
           g.out[o] = v + g.bias[m];
         } else if constexpr (EPI == EP_BIAS_PRIMAL) {
-          g.out[o] = n < g.n_primal ? v + g.bias[m] : v;
-        } else if constexpr (EPI == EP_MUL_DERIV) {
-          g.out[o] = v * g.deriv_in[o];
+          g.out[o] = (n0 + wn * TN * 32 + b * 32 + li) < g.n_primal ? v + g.bias[m] : v;
         } else {  // EP_ACT_*: bias + activation, optionally saving act'(a) for the VJP
           const float z = v + g.bias[m];
           if constexpr (EPI == EP_ACT_SWISH) {

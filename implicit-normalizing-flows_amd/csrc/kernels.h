@@ -98,8 +98,9 @@ int launch_sigma(const float* W, const float* u, const float* v, int cout, int c
 // Packed operand:  dst[(mrow)][kcol] built from W / factor with the given pack mode.
 enum PackMode { PK_ROWMAJOR = 0, PK_TRANSPOSE = 1, PK_IM2COL_FWD = 2, PK_IM2COL_BWD = 3, PK_TAPS_FWD = 4,
                 PK_TAPS_BWD = 5 };
+// frag = 1 writes the fragment-major layout of fused313.hip (Mpad multiple of 32, Kpad of 16).
 int launch_pack(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad, int Kpad,
-                int mode, hipStream_t s);
+                int mode, hipStream_t s, int frag = 0);
 
 // exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
@@ -108,6 +109,30 @@ int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, 
 
 int launch_series_combine(const double* partials, const float* coeff_dev, int n_terms, int batch, int nchunk,
                           float* out, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// fused 3-1-3 conv net (fused313.hip): one launch per forward / derivative-saving forward / VJP
+// ------------------------------------------------------------------------------------------
+enum Net313Mode { MODE_EVAL = 0, MODE_SAVE = 1, MODE_VJP = 2 };
+struct Net313Args {
+  const float* in;        // (B, C, H, W): x (forward) or v (VJP)
+  const float* pre_beta;  // forward: swish preact on `in` (nullptr: none)
+  const float* A1;        // phase A operand, fragment-major (HID x K1pad)
+  int K1pad;
+  const float* A2;        // phase B operand, fragment-major (HID x HID)
+  const float* A3;        // phase C operand, fragment-major (M3pad x HID)
+  int M3, M3pad;          // 9C taps rows
+  const float* b1;
+  const float* beta1;
+  const float* b2;
+  const float* beta2;
+  float* d1;              // (B, HID, H, W) swish'(a1): SAVE writes, VJP reads
+  float* d2;              // (B, HID, H, W) swish'(a2)
+  float* Y;               // (B, M3, H, W) packed taps
+  int B, C, H, W, seg;
+};
+int net313_supported(int hid, int C, int H, int W);
+int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------
 // opt-in launch timing (inf_profile_begin/end): hipEvents around every engine kernel launch,

@@ -455,10 +455,21 @@ int launch_sigma(const float* W, const float* u, const float* v, int cout, int c
 }
 
 __global__ void pack_kernel(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad,
-                            int Kpad, int mode) {
+                            int Kpad, int mode, int frag) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)Mpad * Kpad) return;
-  const int m = i / Kpad, k = i - (long)m * Kpad;
+  int m, k;
+  if (frag) {   // i = ((rb * nkt + kt) * 64 + lane) * 8 + kk  ->  (32 rb + lane&31, 16 kt + 8 (lane>>5) + kk)
+    const int nkt = Kpad / 16;
+    const int kk = i & 7, lane = (i >> 3) & 63;
+    const long tile = i >> 9;
+    const int kt = tile % nkt, rb = tile / nkt;
+    m = rb * 32 + (lane & 31);
+    k = kt * 16 + 8 * (lane >> 5) + kk;
+  } else {
+    m = i / Kpad;
+    k = i - (long)m * Kpad;
+  }
   const float f = factor[0];
   const int kk = ks * ks;
   int co = -1, ci = -1, t = 0;
@@ -473,10 +484,10 @@ __global__ void pack_kernel(const float* W, const float* factor, float* dst, int
   dst[i] = co >= 0 ? W[((long)co * cin + ci) * kk + t] / f : 0.f;
 }
 int launch_pack(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad, int Kpad,
-                int mode, hipStream_t s) {
+                int mode, hipStream_t s, int frag) {
   const long n = (long)Mpad * Kpad;
   hipLaunchKernelGGL(pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, factor, dst, cout, cin, ks, Mpad, Kpad,
-                     mode);
+                     mode, frag);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

@@ -273,6 +273,8 @@ def profile_end():
 
 def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
+    if 500 <= tag < 510:
+        return 'net313_kernel<%s>' % ['EVAL', 'SAVE', 'VJP'][tag - 500]
     if tag < 1000:
         modes = {0: 'PLAIN', 1: 'EMBED', 2: 'RESID', 3: 'RECOMP', 4: 'VJP'}
         return 'conv_out_kernel<%d> mode %s' % (tag % 10, modes.get((tag - 900) // 10, '?'))
