@@ -808,6 +808,67 @@ int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const floa
   return launch_series_combine(bf.part, coeff, n_terms, B, bf.nchunk, out, s);
 }
 
+// Both log-det series of an imBlock (x-branch and z-branch, implicit_block.py:318-322) advanced in
+// lockstep: when both nets take the fused path, every term is ONE launch over both nets' tiles.
+// ws must hold 2 x inf_workspace_bytes(net, batch, 1).
+int inf_logdet_series_pair(InfNet* na, const float* xa, const float* ea, InfNet* nb, const float* xb, const float* eb,
+                           const float* coeff, int n_terms, float* out_a, float* out_b, int B, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!na || !nb || !xa || !xb || !ea || !eb || !coeff || !out_a || !out_b || B <= 0 || n_terms < 0 ||
+      n_terms > SERIES_MAX || !same_shape(na, nb))
+    return INF_ERR_INVALID;
+  const size_t half = ws_need(na, B, 1);
+  if (!ws || ws_bytes < 2 * half) return INF_ERR_WORKSPACE;
+  char* w0 = reinterpret_cast<char*>(ws);
+  if (!(na->fused && nb->fused && na->fhid == nb->fhid)) {
+    INF_TRY(inf_logdet_series(na, xa, ea, coeff, n_terms, out_a, B, w0, half, stream));
+    return inf_logdet_series(nb, xb, eb, coeff, n_terms, out_b, B, w0 + half, half, stream);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bfa, bfb;
+  carve(na, B, 1, w0, half, bfa);
+  carve(nb, B, 1, w0 + half, half, bfb);
+  if (n_terms == 0) {
+    INF_HIP(hipMemsetAsync(out_a, 0, sizeof(float) * B, s));
+    INF_HIP(hipMemsetAsync(out_b, 0, sizeof(float) * B, s));
+    return INF_OK;
+  }
+  Net313Args args[2] = {net313_args(na, xa, B, bfa, false), net313_args(nb, xb, B, bfb, false)};
+  INF_TRY(launch_net313_multi(args, 2, na->fhid, MODE_SAVE, s));
+  const float* va = ea;
+  const float* vb = eb;
+  for (int k = 0; k < n_terms; ++k) {
+    float* oa = (k % 2 == 0) ? bfa.va : bfa.vb;
+    float* ob = (k % 2 == 0) ? bfb.va : bfb.vb;
+    Net313Args vargs[2] = {net313_args(na, va, B, bfa, true), net313_args(nb, vb, B, bfb, true)};
+    INF_TRY(launch_net313_multi(vargs, 2, na->fhid, MODE_VJP, s));
+    for (int i = 0; i < 2; ++i) {
+      InfNet* n = i ? nb : na;
+      Bufs& bf = i ? bfb : bfa;
+      OutArgs a;
+      memset(&a, 0, sizeof(a));
+      a.Y = bf.Y;
+      a.y_sample = (long)n->M3 * n->P;
+      a.C = n->C;
+      a.H = n->H;
+      a.W = n->W;
+      a.ks = 3;
+      a.mode = OM_VJP;
+      a.in0 = i ? eb : ea;
+      a.in1 = i ? xb : xa;
+      a.out0 = i ? ob : oa;
+      a.pre_beta = n->pre_beta;
+      a.partial = bf.part + (size_t)k * B * bf.nchunk;
+      a.nchunk = bf.nchunk;
+      INF_TRY(launch_conv_out(a, B, s));
+    }
+    va = oa;
+    vb = ob;
+  }
+  INF_TRY(launch_series_combine(bfa.part, coeff, n_terms, B, bfa.nchunk, out_a, s));
+  return launch_series_combine(bfb.part, coeff, n_terms, B, bfb.nchunk, out_b, s);
+}
+
 int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,
                        int B, void* ws, size_t ws_bytes, void* stream) {
   if (!n || !x || !vareps || !ncoeff || !out || B <= 0 || n_terms < 0) return INF_ERR_INVALID;

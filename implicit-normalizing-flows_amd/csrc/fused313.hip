@@ -25,7 +25,7 @@
 
 namespace inf {
 
-constexpr int F_BN = 64;          // pixels per tile
+constexpr int F_BN_MAX = 64;      // pixels per tile (64, or 32 for small grids)
 constexpr int F_LDS_FLOATS = 40960;   // 160 KiB
 
 __device__ __forceinline__ void load_frag8(const float* base, float* o) {
@@ -40,9 +40,14 @@ __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;
 }
 
-template <int TM, int MODE>
-__global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
+template <int TM, int MODE, int F_BN>
+__global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   constexpr int HID = 8 * 32 * TM;
+  constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
+  // two independent nets (the x- and z-branch of an imBlock) can share one launch
+  const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
+  const Net313Args& a = pr.a[sel];
+  const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
   float* t = smem;                                  // [HID][64] activation tile
   int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
@@ -52,7 +57,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
   const int li = lane & 31, lh = lane >> 5;
   const int P = a.H * a.W;
   const int tiles_per_img = P / F_BN;
-  const int img = blockIdx.x / tiles_per_img, tile = blockIdx.x - img * tiles_per_img;
+  const int img = bid / tiles_per_img, tile = bid - img * tiles_per_img;
   const int p0 = tile * F_BN;
   // tile geometry: `rows` image rows of `seg` pixels (seg = min(W, 64))
   const int seg = a.seg, rows = F_BN / seg;
@@ -85,9 +90,9 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
     koff[k] = o;
   }
   // pixel offsets of this lane's two columns inside the halo tile, and in the image
-  int pix[2], gp[2];
+  int pix[NB], gp[NB];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < NB; ++b) {
     const int n = b * 32 + li;
     const int py = n / seg, px = n - py * seg;
     pix[b] = py * CW + px;
@@ -104,12 +109,12 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
   auto roff = [&](int r) { return ((r & 3) + 8 * (r >> 2)) * P; };
 
   // VJP: prefetch the phase-A multiplier d2 (retired by the phase-A loop's waits)
-  float dmul[TM][2][16];
+  float dmul[TM][NB][16];
   if constexpr (MODE == MODE_VJP) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NB; ++b) {
           const float* src = hid_base(a.d2, m, b);
 #pragma unroll
           for (int r = 0; r < 16; ++r) dmul[m][b][r] = src[roff(r)];
@@ -117,12 +122,12 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
   }
   __syncthreads();
 
-  f32x16 acc[TM][2];
+  f32x16 acc[TM][NB];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[m][b][r] = 0.f;
   };
@@ -150,12 +155,14 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
       }
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const float b0 = vh[ko[kk] + pix[0]], b1 = vh[ko[kk] + pix[1]];
+        float bv[NB];
 #pragma unroll
-        for (int m = 0; m < TM; ++m) {
-          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b0, acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b1, acc[m][1], 0, 0, 0);
-        }
+        for (int b = 0; b < NB; ++b) bv[b] = vh[ko[kk] + pix[b]];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], bv[b], acc[m][b], 0, 0, 0);
       }
     }
   }
@@ -165,7 +172,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NB; ++b) {
         float* dst = (MODE == MODE_SAVE) ? hid_base(a.d1, m, b) : nullptr;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -200,12 +207,14 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
       const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const float b0 = tb[kk * F_BN], b1 = tb[kk * F_BN + 32];
+        float bv[NB];
 #pragma unroll
-        for (int m = 0; m < TM; ++m) {
-          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b0, acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], b1, acc[m][1], 0, 0, 0);
-        }
+        for (int b = 0; b < NB; ++b) bv[b] = tb[kk * F_BN + 32 * b];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], bv[b], acc[m][b], 0, 0, 0);
       }
     }
   }
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NB; ++b) {
         float* dst = hid_base(a.d2, m, b);
 #pragma unroll
         for (int r = 0; r < 16; ++r) dst[roff(r)] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < NB; ++b)
         {
           const float* src = hid_base(a.d1, m, b);
 #pragma unroll
@@ -238,7 +247,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int o = row_of(m, r);
@@ -249,7 +258,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
     __syncthreads();
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
     // tasks = (32-row block of the M3pad tap rows) x (32-pixel column); split K when there are
     // fewer tasks than waves, partial tiles reduced through LDS.
     const int nrb = a.M3pad / 32;
-    const int ntask = nrb * 2;
+    const int ntask = nrb * NB;
     int ksplit = 1;
     while (ntask * ksplit * 2 <= 8 && ksplit < 8) ksplit *= 2;
     constexpr int nkt = HID / 16;
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
       for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
       if (job >= njobs) continue;
       const int task = job / ksplit, ks = job - task * ksplit;
-      const int rb = task >> 1, b = task & 1;
+      const int rb = task / NB, b = task % NB;
       for (int kt = ks * kts; kt < (ks + 1) * kts; ++kt) {
         float af[8];
         load_frag8(a.A3 + frag_off(rb, kt, nkt, lane), af);
@@ -289,7 +298,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
       for (int jj = 0; jj < 4; ++jj) {
         const int job = wid + 8 * jj;
         if (job >= njobs) continue;
-        const int rb = job >> 1, b = job & 1;
+        const int rb = job / NB, b = job % NB;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
       __syncthreads();
       // one wave per task sums its ksplit partials
       for (int task = wid; task < ntask; task += 8) {
-        const int rb = task >> 1, b = task & 1;
+        const int rb = task / NB, b = task % NB;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float s = 0.f;
@@ -321,46 +330,68 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Args a) {
   }
 }
 
-int net313_supported(int hid, int C, int H, int W) {
-  if (hid != 512 && hid != 256) return 0;
+static int tile_bn(int hid, int C, int H, int W, int bn) {
   const int P = H * W;
-  const int seg = W < F_BN ? W : F_BN;
-  if (P % F_BN != 0 || F_BN % seg != 0 || (W > F_BN && W % F_BN != 0)) return 0;
-  const int rows = F_BN / seg;
+  const int seg = W < bn ? W : bn;
+  if (P % bn != 0 || bn % seg != 0 || (W > bn && W % bn != 0)) return 0;
+  const int rows = bn / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
-  const long need = (long)hid * F_BN + k1pad + (long)C * (rows + 2) * (seg + 2) + 1;
+  const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + 1;
   if (need > F_LDS_FLOATS) return 0;
   const long m3pad = (9L * C + 31) / 32 * 32;
-  if ((m3pad / 32) * 2 > 32) return 0;            // at most 4 phase-C jobs per wave
+  if ((m3pad / 32) * (bn / 32) > 32) return 0;    // at most 4 phase-C jobs per wave
   return 1;
 }
 
-int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s) {
-  if (!net313_supported(hid, a.C, a.H, a.W)) return INF_ERR_UNSUPPORTED;
-  const int P = a.H * a.W;
-  const unsigned nb = (unsigned)(a.B * (P / F_BN));
+int net313_supported(int hid, int C, int H, int W) {
+  if (hid != 512 && hid != 256) return 0;
+  return tile_bn(hid, C, H, W, 64) || tile_bn(hid, C, H, W, 32);
+}
+
+// Launch one or two nets (same shape) as one grid.  The 64-pixel tile is used unless the grid would
+// leave CUs idle (fewer than 256 workgroups), then 32-pixel tiles.
+int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s) {
+  const Net313Args& a0 = args[0];
+  if (!net313_supported(hid, a0.C, a0.H, a0.W) || nnets < 1 || nnets > 2) return INF_ERR_UNSUPPORTED;
+  const int P = a0.H * a0.W;
+  int bn = 64;
+  if (!tile_bn(hid, a0.C, a0.H, a0.W, 64) || (nnets * a0.B * (P / 64) < 256 && tile_bn(hid, a0.C, a0.H, a0.W, 32)))
+    bn = 32;
+  Net313Pair pr;
+  pr.a[0] = args[0];
+  pr.a[1] = args[nnets - 1];
+  for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < bn ? a0.W : bn;
+  pr.nb0 = a0.B * (P / bn);
+  const unsigned nb = (unsigned)(pr.nb0 * nnets);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define L313(TM_, MODE_) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, a)
+#define L313(TM_, MODE_, BN_) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, BN_>), dim3(nb), dim3(512), 0, s, pr)
+#define L313M(TM_, BN_)                                \
+  do {                                                 \
+    if (mode == MODE_EVAL) L313(TM_, MODE_EVAL, BN_);  \
+    else if (mode == MODE_SAVE) L313(TM_, MODE_SAVE, BN_); \
+    else L313(TM_, MODE_VJP, BN_);                     \
+  } while (0)
   if (hid == 512) {
-    if (mode == MODE_EVAL) L313(2, MODE_EVAL);
-    else if (mode == MODE_SAVE) L313(2, MODE_SAVE);
-    else L313(2, MODE_VJP);
+    if (bn == 64) L313M(2, 64); else L313M(2, 32);
   } else {
-    if (mode == MODE_EVAL) L313(1, MODE_EVAL);
-    else if (mode == MODE_SAVE) L313(1, MODE_SAVE);
-    else L313(1, MODE_VJP);
+    if (bn == 64) L313M(1, 64); else L313M(1, 32);
   }
+#undef L313M
 #undef L313
   INF_CHECK_LAUNCH();
   if (prof) {
-    const double npx = (double)a.B * P;
-    const double fA = 2.0 * hid * 9.0 * a.C, fB = 2.0 * hid * hid, fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a.C * hid;
-    const double bytes = 4.0 * npx * (a.C + (mode == MODE_SAVE ? 2.0 * hid : (mode == MODE_VJP ? 2.0 * hid : 0.0)) +
-                                      (mode == MODE_SAVE ? 0.0 : 9.0 * a.C));
+    const double npx = (double)nnets * a0.B * P;
+    const double fA = 2.0 * hid * 9.0 * a0.C, fB = 2.0 * hid * hid;
+    const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
+    const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
     prof_end_launch(s, 500 + mode, npx * (fA + fB + fC), bytes);
   }
   return INF_OK;
+}
+
+int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s) {
+  return launch_net313_multi(&a, 1, hid, mode, s);
 }
 
 }  // namespace inf

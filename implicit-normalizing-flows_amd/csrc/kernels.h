@@ -131,8 +131,13 @@ struct Net313Args {
   float* Y;               // (B, M3, H, W) packed taps
   int B, C, H, W, seg;
 };
+struct Net313Pair {
+  Net313Args a[2];
+  int nb0;                // workgroups of net 0; blocks >= nb0 run net 1
+};
 int net313_supported(int hid, int C, int H, int W);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
+int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------
 // opt-in launch timing (inf_profile_begin/end): hipEvents around every engine kernel launch,

@@ -73,6 +73,8 @@ _SIGS = {
                                           ctypes.c_int, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_series': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                          ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logdet_series_pair': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                              _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_neumann': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                           ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),

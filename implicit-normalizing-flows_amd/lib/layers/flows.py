@@ -107,6 +107,10 @@ class _ActNorm(nn.Module):
         self.bias = nn.Parameter(torch.Tensor(num_features))
         self.register_buffer('initialized', torch.tensor(0))
 
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.__dict__['_init_seen'] = False
+        super()._load_from_state_dict(*args, **kwargs)
+
     def _data_init(self, x):
         with torch.no_grad():
             c = x.size(1)
@@ -117,8 +121,10 @@ class _ActNorm(nn.Module):
             self.initialized.fill_(1)
 
     def forward(self, x, logpx=None, restore=None):
-        if not self.initialized:
-            self._data_init(x)
+        if not self.__dict__.get('_init_seen', False):     # one device read, then cached
+            if not self.initialized:
+                self._data_init(x)
+            self.__dict__['_init_seen'] = True
         B, C = x.shape[0], x.shape[1]
         hw = x[0, 0].numel()
         if x.is_cuda and x.dtype == torch.float32:

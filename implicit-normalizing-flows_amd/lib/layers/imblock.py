@@ -89,10 +89,12 @@ class imBlock(nn.Module):
     def _native(self, t):
         _hip.require_device(t, 'imBlock')
         shape = t.shape[1:]
-        for net in (self.nnet_x, self.nnet_z):
-            if _uninitialised_convs(net):            # lazy u/v sizing on first use (mixed_lipschitz.py:389)
-                with torch.no_grad():
-                    net(t[:1])
+        if not self.__dict__.get('_convs_ready', False):
+            for net in (self.nnet_x, self.nnet_z):
+                if _uninitialised_convs(net):        # lazy u/v sizing on first use (mixed_lipschitz.py:389)
+                    with torch.no_grad():
+                        net(t[:1])
+            self.__dict__['_convs_ready'] = True
         stream = _hip.stream_of(t)
         nets = []
         for net in (self.nnet_x, self.nnet_z):
@@ -154,12 +156,20 @@ class imBlock(nn.Module):
         return x, logpy + self._logdetgrad(z, x)
 
     # ---------------------------------------------------------------------------------------
+    def _host_scalar(self, name, t):
+        """t.item() without a device sync per call: re-read only when the tensor changed."""
+        key = (t.data_ptr(), t._version, t.device)
+        cache = self.__dict__.setdefault('_host_scalars', {})
+        if cache.get(name, (None,))[0] != key:
+            cache[name] = (key, t.item())
+        return cache[name][1]
+
     def _series_plan(self):
         """Series length and coefficient function (implicit_block.py:261-289)."""
         if self.n_dist == 'geometric':
             param = torch.sigmoid(self.geom_p).item()
         elif self.n_dist == 'poisson':
-            param = self.lamb.item()
+            param = self._host_scalar('lamb', self.lamb)
         else:
             raise ValueError(self.n_dist)
         if self.training and self.n_power_series is not None:
@@ -200,10 +210,12 @@ class imBlock(nn.Module):
         else:
             co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
             carr = co.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
-            for i, (net, t, e) in enumerate(((nx, x, vareps_x), (nz, z, vareps_z))):
-                _hip.check(lib.inf_logdet_series(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(e), carr, n_ps,
-                                                 _hip.ptr(out[i]), B, _hip.ptr(ws), ws.numel(), stream),
-                           'inf_logdet_series')
+            # both branches in lockstep: one fused launch per series term for x- and z-nets
+            ws = _hip.workspace(x.device, 2 * max(nx.ws_bytes(B), nz.ws_bytes(B)))
+            xc, zc = x.contiguous(), z.contiguous()
+            _hip.check(lib.inf_logdet_series_pair(nx.handle, _hip.ptr(xc), _hip.ptr(vareps_x), nz.handle, _hip.ptr(zc),
+                                                  _hip.ptr(vareps_z), carr, n_ps, _hip.ptr(out[0]), _hip.ptr(out[1]),
+                                                  B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series_pair')
         logdetgrad = out[0] - out[1]
         self.last_n_power_series = n_ps
         if self.training and self.n_power_series is None:

@@ -115,6 +115,12 @@ int inf_imblock_forward(InfNet* net_x, InfNet* net_z, const float* x, float* z, 
  * (coeff is a HOST array, rounded to fp32 as the reference's scalar*tensor product does). */
 int inf_logdet_series(InfNet* net, const float* x, const float* vareps, const float* coeff, int n_terms,
                       float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* Both series of an imBlock (nnet_x at x, nnet_z at z; implicit_block.py:318-322) in lockstep, one
+ * fused launch per term for both nets when the nets take the fused 3-1-3 path.
+ * ws >= 2 * inf_workspace_bytes(net, batch, 1). */
+int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_a, InfNet* net_b, const float* x_b,
+                           const float* vareps_b, const float* coeff, int n_terms, float* out_a, float* out_b,
+                           int batch, void* ws, size_t ws_bytes, void* stream);
 /* Neumann gradient surrogate value (implicit_block.py:429-438): w = sum_{k=0}^{n} ncoeff[k] (J^T)^k eps,
  * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
 int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,
