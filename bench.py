@@ -81,8 +81,7 @@ def cpu_baseline(arch, sd, model, device, nimg):
 def main():
     args = parse()
     rank, world = dd.init_from_env()
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    device = torch.device('cuda', local)
+    device = torch.device('cuda', dd.local_device_index())
     torch.cuda.set_device(device)
     arch = syn.CONFIGS[args.config]
     B = args.batch

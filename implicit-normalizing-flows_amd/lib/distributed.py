@@ -21,13 +21,19 @@ def init_from_env(backend=None):
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     if ws <= 1 or (dist.is_available() and dist.is_initialized()):
         return world()
-    if backend is None:
-        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+    if backend is None:   # INFLOW_DIST_BACKEND=gloo rehearses several ranks on one device
+        backend = os.environ.get('INFLOW_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-    if backend == 'nccl':
-        torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device_index())
     dist.init_process_group(backend=backend)
     return world()
+
+
+def local_device_index():
+    """LOCAL_RANK, folded onto the visible devices (several rehearsal ranks may share one GPU)."""
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    return int(os.environ.get('LOCAL_RANK', '0')) % max(n, 1)
 
 
 def shard(n_total, rank, world_size):
