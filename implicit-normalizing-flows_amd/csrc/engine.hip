@@ -1040,5 +1040,6 @@ int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* s
   if (!out && n) return INF_ERR_INVALID;
   return glue_rademacher(out, n, seed, offset, (hipStream_t)stream);
 }
+int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
 
 }  // extern "C"

@@ -21,6 +21,8 @@
 // dwordx4 loads per row block (no LDS for A).  B fragments come from LDS: one ds_read2_b32 per
 // MFMA k-step (32 lanes read 32 consecutive floats: conflict-free).
 // 8 waves x (TM*32 rows) cover HID = 256*TM rows; each wave owns 2 x 32 pixel columns.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace inf {
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
   float* t = smem;                                  // [HID][64] activation tile
   int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
-  float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile (+1 zero slot)
+  float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
@@ -64,11 +66,14 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   const int y0 = p0 / a.W, x0 = p0 - y0 * a.W;
   const int RH = rows + 2, CW = seg + 2;
   const int vhn = a.C * RH * CW;
+  // K-padding rows of the im2col point at vh[vhn]; phase A reads vh[koff + pix], so the zero run
+  // after the halo must cover every pixel offset of the tile: rows * CW floats.
+  const int vhz = vhn + rows * CW;
 
   // ---- stage the input halo tile (zero padded; forward applies the preact swish) ----
   const float* in = a.in + (long)img * a.C * P;
   const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
-  for (int i = tid; i <= vhn; i += 512) {
+  for (int i = tid; i < vhz; i += 512) {
     float v = 0.f;
     if (i < vhn) {
       const int c = i / (RH * CW), rr = i - c * RH * CW;
@@ -133,37 +138,44 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   };
 
   // ---------------------------------------------------------------- phase A: K = 9C (im2col)
+  // Static ping-pong A fragments (a runtime-indexed double buffer would make the compiler wait for
+  // the prefetch it just issued); the 8 x NB B values of a K tile are read from LDS in one batch.
   zero_acc();
   {
     const int nkt = a.K1pad / 16;
-    float af[2][TM][8];
+    auto tileA = [&](int kt, const float (&af)[TM][8]) {
+      const int* kp = koff + kt * 16 + lh * 8;
+      const int4 k0 = *reinterpret_cast<const int4*>(kp);
+      const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
+      const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+      float bv[8][NB];
 #pragma unroll
-    for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, 0, nkt, lane), af[0][m]);
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nkt) {
+      for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-        for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, kt + 1, nkt, lane), af[cur ^ 1][m]);
-      }
-      int ko[8];
-      {
-        const int* kp = koff + kt * 16 + lh * 8;
-        const int4 k0 = *reinterpret_cast<const int4*>(kp);
-        const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
-        ko[0] = k0.x; ko[1] = k0.y; ko[2] = k0.z; ko[3] = k0.w;
-        ko[4] = k1.x; ko[5] = k1.y; ko[6] = k1.z; ko[7] = k1.w;
-      }
+        for (int b = 0; b < NB; ++b) bv[kk][b] = vh[ko[kk] + pix[b]];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        float bv[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) bv[b] = vh[ko[kk] + pix[b]];
+      for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
         for (int m = 0; m < TM; ++m)
 #pragma unroll
           for (int b = 0; b < NB; ++b)
-            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], bv[b], acc[m][b], 0, 0, 0);
+            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[m][kk], bv[kk][b], acc[m][b], 0, 0, 0);
+    };
+    float a0[TM][8], a1[TM][8];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, 0, nkt, lane), a0[m]);
+    for (int kt = 0; kt < nkt; kt += 2) {
+      const bool has1 = kt + 1 < nkt;
+      if (has1) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, kt + 1, nkt, lane), a1[m]);
       }
+      tileA(kt, a0);
+      if (kt + 2 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) load_frag8(a.A1 + frag_off(rbw + m, kt + 2, nkt, lane), a0[m]);
+      }
+      if (has1) tileA(kt + 1, a1);
     }
   }
   // epilogue A -> t (LDS); SAVE: d1 -> HBM
@@ -195,27 +207,33 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   zero_acc();
   {
     constexpr int nkt = HID / 16;
-    float af[2][TM][8];
-#pragma unroll
-    for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, 0, nkt, lane), af[0][m]);
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nkt) {
-#pragma unroll
-        for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, kt + 1, nkt, lane), af[cur ^ 1][m]);
-      }
+    auto tileB = [&](int kt, const float (&af)[TM][8]) {
       const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
+      float bv[8][NB];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        float bv[NB];
+      for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) bv[b] = tb[kk * F_BN + 32 * b];
+        for (int b = 0; b < NB; ++b) bv[kk][b] = tb[kk * F_BN + 32 * b];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
         for (int m = 0; m < TM; ++m)
 #pragma unroll
           for (int b = 0; b < NB; ++b)
-            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[cur][m][kk], bv[b], acc[m][b], 0, 0, 0);
+            acc[m][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[m][kk], bv[kk][b], acc[m][b], 0, 0, 0);
+    };
+    float a0[TM][8], a1[TM][8];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, 0, nkt, lane), a0[m]);
+    for (int kt = 0; kt < nkt; kt += 2) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, kt + 1, nkt, lane), a1[m]);
+      tileB(kt, a0);
+      if (kt + 2 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) load_frag8(a.A2 + frag_off(rbw + m, kt + 2, nkt, lane), a0[m]);
       }
+      tileB(kt + 1, a1);
     }
   }
   if constexpr (MODE == MODE_SAVE) {
@@ -269,7 +287,7 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
     const int nrb = a.M3pad / 32;
     const int ntask = nrb * NB;
     int ksplit = 1;
-    while (ntask * ksplit * 2 <= 8 && ksplit < 8) ksplit *= 2;
+    while (ntask * ksplit * 2 <= 8 && ksplit < pr.max_ksplit) ksplit *= 2;
     constexpr int nkt = HID / 16;
     const int kts = nkt / ksplit;
     const int njobs = ntask * ksplit;
@@ -283,13 +301,23 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
       if (job >= njobs) continue;
       const int task = job / ksplit, ks = job - task * ksplit;
       const int rb = task / NB, b = task % NB;
-      for (int kt = ks * kts; kt < (ks + 1) * kts; ++kt) {
-        float af[8];
-        load_frag8(a.A3 + frag_off(rb, kt, nkt, lane), af);
-        const float* tb = t + (kt * 16 + lh * 8) * F_BN + b * 32 + li;
+      const float* tcol = t + lh * 8 * F_BN + b * 32 + li;
+      auto tileC = [&](int kt, const float (&af)[8]) {
+        float bv[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) bv[kk] = tcol[(kt * 16 + kk) * F_BN];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
-          cacc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk], tb[kk * F_BN], cacc[jj], 0, 0, 0);
+          cacc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk], bv[kk], cacc[jj], 0, 0, 0);
+      };
+      const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is even
+      float c0[8], c1[8];
+      load_frag8(a.A3 + frag_off(rb, k_lo, nkt, lane), c0);
+      for (int kt = k_lo; kt < k_hi; kt += 2) {
+        load_frag8(a.A3 + frag_off(rb, kt + 1, nkt, lane), c1);
+        tileC(kt, c0);
+        if (kt + 2 < k_hi) load_frag8(a.A3 + frag_off(rb, kt + 2, nkt, lane), c0);
+        tileC(kt + 1, c1);
       }
     }
     float* Y = a.Y + (long)img * a.M3 * P;
@@ -336,7 +364,7 @@ static int tile_bn(int hid, int C, int H, int W, int bn) {
   if (P % bn != 0 || bn % seg != 0 || (W > bn && W % bn != 0)) return 0;
   const int rows = bn / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
-  const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + 1;
+  const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
   if (need > F_LDS_FLOATS) return 0;
   const long m3pad = (9L * C + 31) / 32 * 32;
   if ((m3pad / 32) * (bn / 32) > 32) return 0;    // at most 4 phase-C jobs per wave
@@ -362,6 +390,12 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   pr.a[1] = args[nnets - 1];
   for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < bn ? a0.W : bn;
   pr.nb0 = a0.B * (P / bn);
+  static const int max_ksplit = [] {
+    const char* ks = getenv("INFLOW_FUSED_KSPLIT");     // debug knob: cap phase C's K split
+    const int v = ks ? atoi(ks) : 8;
+    return v < 1 ? 1 : v;
+  }();
+  pr.max_ksplit = max_ksplit;
   const unsigned nb = (unsigned)(pr.nb0 * nnets);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);

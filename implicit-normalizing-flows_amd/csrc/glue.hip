@@ -164,4 +164,18 @@ int glue_init_tangents(const float* xT, float* ext, int d, int B, hipStream_t s)
   return INF_OK;
 }
 
+// 160 KiB of LDS per workgroup, one workgroup per CU at a time; 8 waves of 4 per CU cover every CU.
+__global__ __launch_bounds__(1024) void poison_lds_kernel(float* sink) {
+  __shared__ float lds[40960];
+  const float nan = __builtin_nanf("");
+  for (int i = threadIdx.x; i < 40960; i += 1024) lds[i] = nan;
+  __syncthreads();
+  if (threadIdx.x == 0 && sink) sink[blockIdx.x] = lds[(blockIdx.x * 97) % 40960];
+}
+int glue_poison_lds(hipStream_t s) {
+  hipLaunchKernelGGL(poison_lds_kernel, dim3(256 * 8), dim3(1024), 0, s, nullptr);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 }  // namespace inf

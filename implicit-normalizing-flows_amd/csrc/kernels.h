@@ -134,6 +134,7 @@ struct Net313Args {
 struct Net313Pair {
   Net313Args a[2];
   int nb0;                // workgroups of net 0; blocks >= nb0 run net 1
+  int max_ksplit;         // cap on phase C's K split (debug knob, INFLOW_FUSED_KSPLIT)
 };
 int net313_supported(int hid, int C, int H, int W);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);

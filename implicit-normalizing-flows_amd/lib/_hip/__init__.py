@@ -85,6 +85,7 @@ _SIGS = {
     'inf_profile_begin': (ctypes.c_int, [ctypes.c_int]),
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
+    'inf_debug_poison_lds': (ctypes.c_int, [_P]),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -155,6 +155,10 @@ typedef struct InfKernelStat {
 int inf_profile_begin(int max_launches);
 int inf_profile_end(InfKernelStat* out, int max_out, int* n_out);
 
+/* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
+ * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
+int inf_debug_poison_lds(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -232,12 +232,14 @@ def test_device_rademacher():
     assert abs(p.mean().item()) < 0.01
 
 
+@pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3, 5])
-def test_fused_313_matches_generic_path(block, monkeypatch):
+def test_fused_313_matches_generic_path(block, B, monkeypatch):
     """The fused 3-1-3 kernel (fused313.hip) and the generic GEMM chain agree on forward, VJP
-    and the log-det series of the full-size CIFAR nets."""
+    and the log-det series of the full-size CIFAR nets.  Before every call the workspace and the
+    LDS of every CU are filled with NaN, so a read of memory the kernels never wrote shows up as
+    NaN deterministically (B=2 takes the 32-pixel split-K tiles, B=16 the 64-pixel tiles)."""
     arch = syn.CIFAR10
-    B = 2
     outs = {}
     for mode in ('fused', 'generic'):
         monkeypatch.setenv('INFLOW_NO_FUSED', '1' if mode == 'generic' else '0')
@@ -252,19 +254,28 @@ def test_fused_313_matches_generic_path(block, monkeypatch):
         stream = _hip.stream_of(x)
         net.refresh_if_needed(stream)
         ws = _hip.workspace(x.device, net.ws_bytes(B))
+
+        def poison():
+            ws.fill_(255)
+            _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
         y = torch.empty_like(x)
         g = torch.empty_like(x)
+        poison()
         _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
                                            stream), 'fwd')
+        poison()
         _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(x), _hip.ptr(v), _hip.ptr(g), B, _hip.ptr(ws),
                                        ws.numel(), stream), 'vjp')
         co = np.array([(-1) ** (k + 1) / k for k in range(1, 11)], dtype=np.float32)
         ld = torch.empty(B, device=DEV)
         eps = torch.sign(v)
+        poison()
         _hip.check(net.lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(eps),
                                              co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 10, _hip.ptr(ld), B,
                                              _hip.ptr(ws), ws.numel(), stream), 'series')
         torch.cuda.synchronize()
         outs[mode] = (y, g, ld)
+    for a in outs['fused']:
+        assert torch.isfinite(a).all()
     for a, b in zip(outs['fused'], outs['generic']):
         _close(a, b, rel=1e-5)
