@@ -119,7 +119,9 @@ struct Bufs {
   float *ext0, *ext1;
   double *part, *bpart, *sumsq;
   unsigned int* counter;
-  int nchunk;
+  int nchunk;              // per-sample partial chunks of conv_out (residual norms, unfused series)
+  float* Y2;               // fused nets: second taps buffer (series terms alternate Y / Y2)
+  int snchunk;             // per-sample partial stride of the series slabs (>= tiles per image)
 };
 
 size_t per_sample_hidden(const InfNet* n) { return (size_t)n->hidden_max * (n->fc ? 1 : n->P); }
@@ -134,9 +136,11 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   const size_t Ys = (size_t)B * n->rows_max * (n->fc ? 1 : n->P);
   const int nchunk = n->fc ? 1 : out_nchunk(n->d);
   b.nchunk = nchunk;
+  b.snchunk = n->fused ? std::max(nchunk, n->P / 32) : nchunk;
   b.h0 = w.take<float>(Hs);
   b.h1 = w.take<float>(Hs);
   b.Y = w.take<float>(Ys);
+  b.Y2 = n->fused ? w.take<float>(Ys) : nullptr;
   b.D.resize(n->L.size() > 0 ? n->L.size() - 1 : 0);
   for (auto& p : b.D) p = w.take<float>(Hs);
   float** vecs[] = {&b.xin, &b.xemb, &b.fx, &b.xa, &b.xb, &b.ga, &b.gb, &b.upd,
@@ -151,7 +155,7 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   } else {
     b.ext0 = b.ext1 = nullptr;
   }
-  b.part = w.take<double>((size_t)B * nchunk * SERIES_MAX);
+  b.part = w.take<double>((size_t)B * std::max(nchunk, b.snchunk) * SERIES_MAX);
   const int bch = (n->d + 1023) / 1024;
   b.bpart = w.take<double>((size_t)B * bch * (3 * (size_t)T + 2) + 64);
   b.sumsq = w.take<double>((size_t)B);
@@ -783,6 +787,63 @@ int inf_imblock_forward(InfNet* nx, InfNet* nz, const float* x, float* z, int B,
   return INF_OK;
 }
 
+// Power series of 1 or 2 fused nets of the same shape (the x- and z-branch of an imBlock advance in
+// lockstep: one launch per term over both nets' tiles).  Term k's VJP stages term k-1's packed taps
+// directly (tap sum, preact swish', trace partial -- conv_out's work), so a term is ONE launch; only
+// the last term's taps go through conv_out.  Series slabs: part[k][b][snchunk] (zeroed first: the
+// fused kernel fills one entry per tile, conv_out one per 1024-element chunk).
+int series_fused(InfNet* const* nets, const float* const* xs, const float* const* es, int nn, const float* coeff,
+                 int n_terms, float* const* outs, int B, Bufs* bfs, hipStream_t s) {
+  Net313Args args[2];
+  for (int i = 0; i < nn; ++i) {
+    args[i] = net313_args(nets[i], xs[i], B, bfs[i], false);
+    INF_HIP(hipMemsetAsync(bfs[i].part, 0, sizeof(double) * n_terms * B * bfs[i].snchunk, s));
+  }
+  INF_TRY(launch_net313_multi(args, nn, nets[0]->fhid, MODE_SAVE, s));
+  for (int k = 0; k < n_terms; ++k) {
+    for (int i = 0; i < nn; ++i) {
+      InfNet* n = nets[i];
+      Bufs& bf = bfs[i];
+      Net313Args& v = args[i];
+      v = net313_args(n, es[i], B, bf, true);
+      v.Y = (k % 2 == 0) ? bf.Y : bf.Y2;
+      if (k > 0) {
+        v.in = nullptr;
+        v.in_taps = (k % 2 == 1) ? bf.Y : bf.Y2;
+        v.vmul_x = n->pre_beta ? xs[i] : nullptr;
+        v.vmul_beta = n->pre_beta;
+        v.dot_eps = es[i];
+        v.dot_part = bf.part + (size_t)(k - 1) * B * bf.snchunk;
+        v.dot_nchunk = bf.snchunk;
+      }
+    }
+    INF_TRY(launch_net313_multi(args, nn, nets[0]->fhid, MODE_VJP, s));
+  }
+  for (int i = 0; i < nn; ++i) {
+    InfNet* n = nets[i];
+    Bufs& bf = bfs[i];
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Y = ((n_terms - 1) % 2 == 0) ? bf.Y : bf.Y2;
+    a.y_sample = (long)n->M3 * n->P;
+    a.C = n->C;
+    a.H = n->H;
+    a.W = n->W;
+    a.ks = 3;
+    a.mode = OM_VJP;
+    a.in0 = es[i];
+    a.in1 = xs[i];
+    a.out0 = bf.va;
+    a.pre_beta = n->pre_beta;
+    a.partial = bf.part + (size_t)(n_terms - 1) * B * bf.snchunk;
+    a.nchunk = bf.snchunk;
+    INF_TRY(launch_conv_out(a, B, s));
+  }
+  for (int i = 0; i < nn; ++i)
+    INF_TRY(launch_series_combine(bfs[i].part, coeff, n_terms, B, bfs[i].snchunk, outs[i], s));
+  return INF_OK;
+}
+
 int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
                       int B, void* ws, size_t ws_bytes, void* stream) {
   if (!n || !x || !vareps || !coeff || !out || B <= 0 || n_terms < 0 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
@@ -798,6 +859,7 @@ int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const floa
   INF_TRY(st);
   const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
   INF_TRY(st);
+  if (n->fused) return series_fused(&n, &xi, &ei, 1, coeff, n_terms, &out, B, &bf, s);
   INF_TRY(run_forward(n, xi, B, bf, -1, nullptr, s));
   const float* v = ei;
   for (int k = 0; k < n_terms; ++k) {
@@ -833,40 +895,12 @@ int inf_logdet_series_pair(InfNet* na, const float* xa, const float* ea, InfNet*
     INF_HIP(hipMemsetAsync(out_b, 0, sizeof(float) * B, s));
     return INF_OK;
   }
-  Net313Args args[2] = {net313_args(na, xa, B, bfa, false), net313_args(nb, xb, B, bfb, false)};
-  INF_TRY(launch_net313_multi(args, 2, na->fhid, MODE_SAVE, s));
-  const float* va = ea;
-  const float* vb = eb;
-  for (int k = 0; k < n_terms; ++k) {
-    float* oa = (k % 2 == 0) ? bfa.va : bfa.vb;
-    float* ob = (k % 2 == 0) ? bfb.va : bfb.vb;
-    Net313Args vargs[2] = {net313_args(na, va, B, bfa, true), net313_args(nb, vb, B, bfb, true)};
-    INF_TRY(launch_net313_multi(vargs, 2, na->fhid, MODE_VJP, s));
-    for (int i = 0; i < 2; ++i) {
-      InfNet* n = i ? nb : na;
-      Bufs& bf = i ? bfb : bfa;
-      OutArgs a;
-      memset(&a, 0, sizeof(a));
-      a.Y = bf.Y;
-      a.y_sample = (long)n->M3 * n->P;
-      a.C = n->C;
-      a.H = n->H;
-      a.W = n->W;
-      a.ks = 3;
-      a.mode = OM_VJP;
-      a.in0 = i ? eb : ea;
-      a.in1 = i ? xb : xa;
-      a.out0 = i ? ob : oa;
-      a.pre_beta = n->pre_beta;
-      a.partial = bf.part + (size_t)k * B * bf.nchunk;
-      a.nchunk = bf.nchunk;
-      INF_TRY(launch_conv_out(a, B, s));
-    }
-    va = oa;
-    vb = ob;
-  }
-  INF_TRY(launch_series_combine(bfa.part, coeff, n_terms, B, bfa.nchunk, out_a, s));
-  return launch_series_combine(bfb.part, coeff, n_terms, B, bfb.nchunk, out_b, s);
+  InfNet* nets[2] = {na, nb};
+  const float* xs[2] = {xa, xb};
+  const float* es[2] = {ea, eb};
+  float* outs[2] = {out_a, out_b};
+  Bufs bfs[2] = {bfa, bfb};
+  return series_fused(nets, xs, es, 2, coeff, n_terms, outs, B, bfs, s);
 }
 
 int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,

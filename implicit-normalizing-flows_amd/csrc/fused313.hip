@@ -28,7 +28,11 @@
 namespace inf {
 
 constexpr int F_BN_MAX = 64;      // pixels per tile (64, or 32 for small grids)
-constexpr int F_LDS_FLOATS = 40960;   // 160 KiB
+// LDS per workgroup: 64-pixel tiles take the whole 160 KiB (one workgroup per CU); 32-pixel tiles
+// take 80 KiB so two workgroups share a CU and overlap each other's staging / epilogues / barriers.
+template <int F_BN>
+constexpr int lds_floats() { return F_BN == 64 ? 40960 : 20480; }
+constexpr int lds_floats_rt(int bn) { return bn == 64 ? 40960 : 20480; }
 
 __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   const f32x4 v0 = *reinterpret_cast<const f32x4*>(base);
@@ -43,7 +47,8 @@ __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
 }
 
 template <int TM, int MODE, int F_BN>
-__global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
+__device__ __forceinline__ void net313_body(const Net313Pair& pr) {
+  constexpr int F_LDS_FLOATS = lds_floats<F_BN>();
   constexpr int HID = 8 * 32 * TM;
   constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
   // two independent nets (the x- and z-branch of an imBlock) can share one launch
@@ -71,20 +76,77 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
   const int vhz = vhn + rows * CW;
 
   // ---- stage the input halo tile (zero padded; forward applies the preact swish) ----
+  // Series chaining: the input is the previous VJP's packed taps; the tap sum, the preact swish'
+  // multiplier and that term's trace partial (conv_out's OM_VJP work) happen here instead.
   const float* in = a.in + (long)img * a.C * P;
   const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
-  for (int i = tid; i < vhz; i += 512) {
-    float v = 0.f;
-    if (i < vhn) {
-      const int c = i / (RH * CW), rr = i - c * RH * CW;
-      const int hy = rr / CW, hx = rr - hy * CW;
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-        v = in[(long)c * P + yy * a.W + xx];
-        if (a.pre_beta) v = swish_f(v, pre_sp);
+  double dacc = 0.0;
+  if (a.in_taps) {
+    const float* ytap = a.in_taps + (long)img * a.M3 * P;
+    const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
+    const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
+    const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
+    // 4 halo elements per pass with unconditional (clamped-address) loads: 36 tap loads in flight
+    // per thread instead of one bounds-checked chain per element.
+    constexpr int SU = 4;
+    for (int i0 = tid; i0 < vhz; i0 += 512 * SU) {
+      float tv[SU][9], xm[SU], ev[SU];
+      int ok[SU];
+      long ee[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = i0 + u * 512;
+        const int ic = i < vhn ? i : 0;
+        const int c = ic / (RH * CW), rr = ic - c * RH * CW;
+        const int hy = rr / CW, hx = rr - hy * CW;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+        ok[u] = in_img ? ((hy >= 1 && hy <= rows && hx >= 1 && hx <= seg) ? 2 : 1) : 0;
+        const int yq = min(max(yy, 0), a.H - 1), xq = min(max(xx, 0), a.W - 1);
+        ee[u] = (long)c * P + yq * a.W + xq;
+        const float* yc = ytap + (long)c * 9 * P;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const int y2 = yq + tp / 3 - 1, x2 = xq + tp % 3 - 1;
+          const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
+          const float val = yc[(long)tp * P + min(max(y2, 0), a.H - 1) * a.W + min(max(x2, 0), a.W - 1)];
+          tv[u][tp] = vt ? val : 0.f;
+        }
+        xm[u] = mx ? mx[ee[u]] : 1.f;
+        ev[u] = ep ? ep[ee[u]] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = i0 + u * 512;
+        float v = 0.f;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) v += tv[u][tp];
+        if (mx) v = v * swish_d(xm[u], msp);
+        v = ok[u] ? v : 0.f;
+        if (ep && ok[u] == 2) dacc += (double)v * (double)ev[u];
+        if (i < vhz) vh[i] = v;
       }
     }
-    vh[i] = v;
+  } else {
+    for (int i = tid; i < vhz; i += 512) {
+      float v = 0.f;
+      if (i < vhn) {
+        const int c = i / (RH * CW), rr = i - c * RH * CW;
+        const int hy = rr / CW, hx = rr - hy * CW;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+          v = in[(long)c * P + yy * a.W + xx];
+          if (a.pre_beta) v = swish_f(v, pre_sp);
+        }
+      }
+      vh[i] = v;
+    }
+  }
+  // per-tile trace partial: wave sums -> a reserved LDS slot at the end of the LDS (never reused)
+  double* red = reinterpret_cast<double*>(smem + F_LDS_FLOATS - 16);
+  if (a.dot_part) {
+    const double w = wave_sum(dacc);
+    if (lane == 0) red[wid] = w;
   }
   for (int k = tid; k < a.K1pad; k += 512) {
     int o = vhn;                                    // zero slot for the K padding
@@ -103,6 +165,12 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
     pix[b] = py * CW + px;
     gp[b] = (y0 + py) * a.W + x0 + px;
   }
+  // gp for a runtime column index (phase C tasks): arithmetic, not gp[b] (which would live in scratch)
+  auto gp_rt = [&](int b) {
+    const int n = b * 32 + li;
+    const int py = n / seg;
+    return (y0 + py) * a.W + x0 + (n - py * seg);
+  };
   const long plane = (long)img * HID * P;           // sample offset of HID-channel tensors
   const int rbw = wid * TM;                          // this wave's first 32-row block
   auto row_of = [&](int m, int r) { return (rbw + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh; };
@@ -126,6 +194,12 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
       }
   }
   __syncthreads();
+  if (a.dot_part && tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s += red[w];
+    a.dot_part[(long)img * a.dot_nchunk + tile] = s;
+  }
 
   f32x16 acc[TM][NB];
   auto zero_acc = [&]() {
@@ -327,10 +401,11 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
         const int job = wid + 8 * jj;
         if (job >= njobs) continue;
         const int rb = job / NB, b = job % NB;
+        const int gcol = gp_rt(b);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.M3) Y[(long)row * P + gp[b]] = cacc[jj][r];
+          if (row < a.M3) Y[(long)row * P + gcol] = cacc[jj][r];
         }
       }
     } else {
@@ -346,16 +421,27 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
       // one wave per task sums its ksplit partials
       for (int task = wid; task < ntask; task += 8) {
         const int rb = task / NB, b = task % NB;
+        const int gcol = gp_rt(b);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float s = 0.f;
           for (int ks = 0; ks < ksplit; ++ks) s += part[((task * ksplit + ks) * 16 + r) * 64 + lane];
           const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.M3) Y[(long)row * P + gp[b]] = s;
+          if (row < a.M3) Y[(long)row * P + gcol] = s;
         }
       }
     }
   }
+}
+
+template <int TM, int MODE>
+__global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
+  net313_body<TM, MODE, 64>(pr);
+}
+// two workgroups (16 waves) per CU: at most 128 VGPRs
+template <int TM, int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void net313_kernel_h(Net313Pair pr) {
+  net313_body<TM, MODE, 32>(pr);
 }
 
 static int tile_bn(int hid, int C, int H, int W, int bn) {
@@ -365,7 +451,7 @@ static int tile_bn(int hid, int C, int H, int W, int bn) {
   const int rows = bn / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
   const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
-  if (need > F_LDS_FLOATS) return 0;
+  if (need > lds_floats_rt(bn) - 16) return 0;            // last 16 floats: trace-partial slots
   const long m3pad = (9L * C + 31) / 32 * 32;
   if ((m3pad / 32) * (bn / 32) > 32) return 0;    // at most 4 phase-C jobs per wave
   return 1;
@@ -382,9 +468,14 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const Net313Args& a0 = args[0];
   if (!net313_supported(hid, a0.C, a0.H, a0.W) || nnets < 1 || nnets > 2) return INF_ERR_UNSUPPORTED;
   const int P = a0.H * a0.W;
+  static const int force_bn = [] {
+    const char* e = getenv("INFLOW_FUSED_BN");            // tuning knob: 32 / 64 (default: auto)
+    return e ? atoi(e) : 0;
+  }();
   int bn = 64;
   if (!tile_bn(hid, a0.C, a0.H, a0.W, 64) || (nnets * a0.B * (P / 64) < 256 && tile_bn(hid, a0.C, a0.H, a0.W, 32)))
     bn = 32;
+  if (force_bn && tile_bn(hid, a0.C, a0.H, a0.W, force_bn)) bn = force_bn;
   Net313Pair pr;
   pr.a[0] = args[0];
   pr.a[1] = args[nnets - 1];
@@ -399,7 +490,11 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const unsigned nb = (unsigned)(pr.nb0 * nnets);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define L313(TM_, MODE_, BN_) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, BN_>), dim3(nb), dim3(512), 0, s, pr)
+#define L313(TM_, MODE_, BN_)                                                                   \
+  do {                                                                                          \
+    if (BN_ == 64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr); \
+    else hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);         \
+  } while (0)
 #define L313M(TM_, BN_)                                \
   do {                                                 \
     if (mode == MODE_EVAL) L313(TM_, MODE_EVAL, BN_);  \
@@ -419,7 +514,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     const double fA = 2.0 * hid * 9.0 * a0.C, fB = 2.0 * hid * hid;
     const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
     const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
-    prof_end_launch(s, 500 + mode, npx * (fA + fB + fC), bytes);
+    prof_end_launch(s, 500 + (bn == 32 ? 10 : 0) + mode, npx * (fA + fB + fC), bytes);   // 51x: 2-per-CU variant
   }
   return INF_OK;
 }

@@ -130,6 +130,14 @@ struct Net313Args {
   float* d2;              // (B, HID, H, W) swish'(a2)
   float* Y;               // (B, M3, H, W) packed taps
   int B, C, H, W, seg;
+  // VJP series chaining (conv_out folded into the next term's halo staging):
+  const float* in_taps;   // non-null: the input v is the previous term's packed taps (B, M3, H, W),
+                          // v = sum of the 9 shifted taps (zero padded), replaces `in`
+  const float* vmul_x;    // with in_taps on preact nets: v *= swish'(vmul_x) (beta vmul_beta)
+  const float* vmul_beta;
+  const float* dot_eps;   // with in_taps: dot_part[img * dot_nchunk + tile] = sum over the tile's own
+  double* dot_part;       //   pixels of v * dot_eps (fp64), the previous term's trace partial
+  int dot_nchunk;
 };
 struct Net313Pair {
   Net313Args a[2];

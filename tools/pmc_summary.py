@@ -35,12 +35,12 @@ def main():
         hbm = 2 * fetch + write
         rows.append({'kernel': k[0], 'grid_threads': k[1], 'dispatches': len(f[k]), 'fetch_size_bytes': fetch,
                      'write_size_bytes': write, 'hbm_bytes_corrected': hbm})
-        if 'net313_kernel<2, 2,' in k[0]:
+        if 'net313_kernel<2, 2>' in k[0]:        # tag 502 (64-pixel tiles); the _h variant is tag 512
             vjp += [hbm] * len(f[k])
     res = {'tag': 502, 'kernel': 'net313_kernel<VJP>', 'batch': a.batch,
            'hbm_bytes_per_launch': sum(vjp) / len(vjp) if vjp else None,
            'method': '2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch, separate --pmc passes, averaged over the '
-                     'VJP dispatches of one bench step (all three scales)', 'per_config': rows}
+                     'net313_kernel<2, 2> (64-pixel-tile VJP) dispatches of the bench run', 'per_config': rows}
     json.dump(res, open(a.out, 'w'), indent=1)
     print(json.dumps({k: res[k] for k in ('kernel', 'batch', 'hbm_bytes_per_launch')}))
 
