@@ -930,12 +930,9 @@ int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const flo
   return launch_series_combine(bf.part, &one, 1, B, bf.nchunk, out, s);
 }
 
-int inf_logdet_exact(InfNet* n, const float* x, float* out, int B, void* ws, size_t ws_bytes, void* stream) {
-  if (!n || !x || !out || B <= 0) return INF_ERR_INVALID;
-  if (!n->fc || n->d > 16 || n->pre_act != ACT_NONE) return INF_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
-  Bufs bf;
-  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+// Forward-mode Jacobian of a small fc net: [primal | d tangents] pushed through every layer; returns
+// the tangent block (J[i][j] of sample b at t[i*(d+1)*B + (j+1)*B + b]) in *tang.
+static int fc_jacobian(InfNet* n, const float* x, int B, Bufs& bf, const float** tang, hipStream_t s) {
   const int d = n->d;
   int st = INF_OK;
   const float* xi = to_internal(n, x, bf.xin, B, s, &st);
@@ -966,7 +963,31 @@ int inf_logdet_exact(InfNet* n, const float* x, float* out, int B, void* ws, siz
     if (w.act != ACT_NONE) INF_TRY(launch_fwdmode_act(o, nullptr, w.cout, B, d, w.act, w.act_beta, s));
     cur = o;
   }
-  return launch_logdet_small(cur, out, d, B, B, s);
+  *tang = cur;
+  return INF_OK;
+}
+
+int inf_logdet_exact(InfNet* n, const float* x, float* out, int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !out || B <= 0) return INF_ERR_INVALID;
+  if (!n->fc || n->d > 16 || n->pre_act != ACT_NONE) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const float* tang = nullptr;
+  INF_TRY(fc_jacobian(n, x, B, bf, &tang, s));
+  return launch_logdet_small(tang, out, n->d, B, B, s);
+}
+
+int inf_logdet_exact_trace(InfNet* n, const float* x, const float* coeff, int n_terms, float* out, int B, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!n || !x || !coeff || !out || B <= 0 || n_terms < 1 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
+  if (!n->fc || n->d > 16 || n->pre_act != ACT_NONE) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  const float* tang = nullptr;
+  INF_TRY(fc_jacobian(n, x, B, bf, &tang, s));
+  return launch_trace_series(tang, coeff, n_terms, out, n->d, B, B, s);
 }
 
 size_t inf_broyden_workspace_bytes(int batch, int d, int threshold) {

@@ -9,6 +9,11 @@ namespace inf {
 
 constexpr int OUT_CH = 1024;   // elements per block in conv_out (256 threads x 4)
 
+// power-series coefficients, passed by value as a kernel argument
+struct CoeffTable {
+  float c[128];
+};
+
 int out_nchunk(int per_sample) { return (per_sample + OUT_CH - 1) / OUT_CH; }
 
 // ------------------------------------------------------------------------------------------
@@ -533,6 +538,51 @@ int launch_logdet_small(const float* tang, float* out, int d, int batch, long st
   return INF_OK;
 }
 
+// Exact-trace power series (implicit_block.py:323-343, iresblock.py:150-157), one thread per sample:
+//   out = tr(J) + sum_{k=2..n} c_k tr(J^k),  J^k = J @ J^(k-1)   (torch.bmm(J, J_k) order)
+// with c_k = (-1)^(k+1)/k * coeff_fn(k) (coeff[k-1]; coeff[0] unused: the reference's first term is
+// the bare trace).  fp32 throughout, accumulated in k order like the reference.
+__global__ void trace_series_kernel(const float* tang, CoeffTable ct, int n_terms, float* out, int d, int batch,
+                                    long stride_j) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  float J[16][16], Pk[16][16];
+  const long ld = (long)(d + 1) * stride_j;
+  float acc = 0.f;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      J[i][j] = tang[i * ld + (j + 1) * stride_j + b];
+      Pk[i][j] = J[i][j];
+    }
+  for (int i = 0; i < d; ++i) acc += J[i][i];
+  for (int k = 2; k <= n_terms; ++k) {
+    float T[16][16];
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        float s = 0.f;
+        for (int m = 0; m < d; ++m) s = fmaf(J[i][m], Pk[m][j], s);
+        T[i][j] = s;
+      }
+    float tr = 0.f;
+    for (int i = 0; i < d; ++i) {
+      for (int j = 0; j < d; ++j) Pk[i][j] = T[i][j];
+      tr += Pk[i][i];
+    }
+    acc = acc + ct.c[k - 1] * tr;
+  }
+  out[b] = acc;
+}
+int launch_trace_series(const float* tang, const float* coeff_host, int n_terms, float* out, int d, int batch,
+                        long stride_j, hipStream_t s) {
+  if (d > 16 || n_terms > 128) return INF_ERR_UNSUPPORTED;
+  CoeffTable ct;
+  for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
+  hipLaunchKernelGGL(trace_series_kernel, dim3((batch + 127) / 128), dim3(128), 0, s, tang, ct, n_terms, out, d,
+                     batch, stride_j);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // forward-mode activation on [primal | ntang tangent blocks], feature-major (d_out, (1+ntang)*B):
 // primal a -> act(a), tangents t -> act'(a) * t.
 __global__ void fwdmode_act_kernel(float* a, int d_out, int batch, int ntang, int act, const float* beta) {
@@ -570,9 +620,6 @@ int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, 
 // power-series combine: tr_k[b] = (float) sum_chunks partial[k][b][c];  out[b] = sum_k fl(c_k * tr_k)
 // accumulated in fp32 in k order like `logdetgrad = logdetgrad + delta` (implicit_block.py:421-426).
 // ------------------------------------------------------------------------------------------
-struct CoeffTable {
-  float c[128];
-};
 __global__ void series_combine_kernel(const double* partials, CoeffTable ct, int n_terms, int batch, int nchunk,
                                       float* out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;

@@ -78,6 +78,8 @@ _SIGS = {
     'inf_logdet_neumann': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                           ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_logdet_exact_trace': (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, ctypes.c_int,
+                                              _P, ctypes.c_size_t, _P]),
     'inf_logit_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_float, _P]),
     'inf_actnorm_forward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),
     'inf_squeeze2': (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]),

@@ -30,7 +30,7 @@ def build_flow(arch, batch=64):
         return torch.nn.Sequential(*mods)
 
     blocks = [layers.imBlock(build_nnet(), build_nnet(), n_dist=arch['n_dist'], n_power_series=None,
-                             exact_trace=False, brute_force=arch['brute_force'], n_samples=1,
+                             exact_trace=arch.get('exact_trace', False), brute_force=arch['brute_force'], n_samples=1,
                              n_exact_terms=arch['n_exact_terms'], neumann_grad=False, grad_in_forward=False,
                              eps_forward=arch['eps_forward'])
               for _ in range(arch['n_blocks'])]

@@ -9,6 +9,7 @@ MI355X engine:
   * power-series log-det      -> inf_logdet_series    (basic_logdet_estimator, :418-426)
   * Neumann surrogate value   -> inf_logdet_neumann   (:429-438, train mode)
   * exact small log-det       -> inf_logdet_exact     (d <= 10 in eval / brute_force, :249-260)
+  * exact-trace power series  -> inf_logdet_exact_trace (exact_trace=True, fc nets, :323-343)
 
 Host work is only what the reference does on the host: the series-length draw (numpy global
 RNG) and, in the default ``'reference'`` probe mode, the Rademacher probes from torch's CPU
@@ -189,10 +190,13 @@ class imBlock(nn.Module):
                 _hip.check(lib.inf_logdet_exact(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(out[i]), B,
                                                 _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_exact')
             return (out[0] - out[1]).view(-1, 1)
-        if self.exact_trace:
-            raise NotImplementedError('exact_trace=True (batch_jacobian power series, implicit_block.py:323-343) '
-                                      'is not implemented on the MI355X engine')
         n_ps, coeff_fn, ns = self._series_plan()
+        if self.exact_trace:     # exact Jacobian traces, fc nets (implicit_block.py:323-343); no probes drawn
+            if x.dim() != 2:
+                raise NotImplementedError('exact_trace=True needs the full Jacobian; supported for fc nets (d <= 16)')
+            logdetgrad = (solvers.exact_trace_logdet(nx, x, n_ps, coeff_fn, stream) -
+                          solvers.exact_trace_logdet(nz, z, n_ps, coeff_fn, stream))
+            return self._finish_logdet(logdetgrad, n_ps, ns)
         vareps_x = _probes(x.shape, x.device)
         vareps_z = _probes(z.shape, z.device)
         ws = _hip.workspace(x.device, max(nx.ws_bytes(B), nz.ws_bytes(B)))
@@ -216,7 +220,10 @@ class imBlock(nn.Module):
             _hip.check(lib.inf_logdet_series_pair(nx.handle, _hip.ptr(xc), _hip.ptr(vareps_x), nz.handle, _hip.ptr(zc),
                                                   _hip.ptr(vareps_z), carr, n_ps, _hip.ptr(out[0]), _hip.ptr(out[1]),
                                                   B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series_pair')
-        logdetgrad = out[0] - out[1]
+        return self._finish_logdet(out[0] - out[1], n_ps, ns)
+
+    def _finish_logdet(self, logdetgrad, n_ps, ns):
+        """Moment buffers in training (implicit_block.py:345-349); returns (B, 1)."""
         self.last_n_power_series = n_ps
         if self.training and self.n_power_series is None:
             self.last_n_samples.copy_(torch.as_tensor(np.asarray(ns)).to(self.last_n_samples))

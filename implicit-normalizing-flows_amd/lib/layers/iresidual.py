@@ -90,14 +90,17 @@ class iResBlock(nn.Module):
             _hip.check(lib.inf_logdet_exact(net.handle, _hip.ptr(x), _hip.ptr(out), B, _hip.ptr(ws), ws.numel(),
                                             stream), 'inf_logdet_exact')
             return out.view(-1, 1)
-        if self.exact_trace:
-            raise NotImplementedError('exact_trace=True is not implemented on the MI355X engine')
         param = torch.sigmoid(self.geom_p).item() if self.n_dist == 'geometric' else self.lamb.item()
+        ns = None
         if self.training and self.n_power_series is not None:
             n_ps, coeff_fn = self.n_power_series, (lambda k: 1.)
         else:
             n_exact = self.n_exact_terms if self.training else 20
-            n_ps, coeff_fn, _ = solvers.series_coefficients(self.n_dist, param, n_exact, self.n_samples)
+            n_ps, coeff_fn, ns = solvers.series_coefficients(self.n_dist, param, n_exact, self.n_samples)
+        if self.exact_trace:     # iresblock.py:146-157 (fc nets, d <= 16)
+            if x.dim() != 2:
+                raise NotImplementedError('exact_trace=True needs the full Jacobian; supported for fc nets (d <= 16)')
+            return self._moments(solvers.exact_trace_logdet(net, x, n_ps, coeff_fn, stream), ns).view(-1, 1)
         vareps = torch.randn_like(x)
         if self.training and self.neumann_grad:
             nco = np.array([1.] + [(-1) ** k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
@@ -109,7 +112,15 @@ class iResBlock(nn.Module):
             _hip.check(lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(vareps),
                                              co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(out),
                                              B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series')
-        return out.view(-1, 1)
+        return self._moments(out, ns).view(-1, 1)
+
+    def _moments(self, logdetgrad, ns):
+        """Moment buffers in training (iresblock.py:159-163)."""
+        if self.training and self.n_power_series is None and ns is not None:
+            self.last_n_samples.copy_(torch.as_tensor(np.asarray(ns)).to(self.last_n_samples))
+            self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
+            self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
+        return logdetgrad
 
     def extra_repr(self):
         return 'dist={}, n_samples={}, n_power_series={}, neumann_grad={}, exact_trace={}, brute_force={}'.format(

@@ -8,6 +8,7 @@ g-evaluations are fused GEMM chains.  The series-length distributions and coeffi
 are host scalar code (numpy global RNG, exactly like the reference, so seeds replay).
 The autograd-based estimators are kept for callers that pass their own graph.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -140,6 +141,22 @@ def series_coefficients(n_dist, p_or_lamb, n_exact, n_samples=1):
     n_ps = int(max(ns)) + n_exact
     coeff_fn = lambda k: 1 / rcdf(k) * sum(ns >= k - n_exact) / len(ns)
     return n_ps, coeff_fn, ns
+
+
+def exact_trace_logdet(net, x, n_ps, coeff_fn, stream):
+    """Exact-trace power series of one fc net (implicit_block.py:323-343, iresblock.py:150-157):
+    tr(J) + sum_{k>=2} (-1)^(k+1)/k coeff_fn(k) tr(J^k) per sample -> (B,) on the device."""
+    B = x.shape[0]
+    co = np.zeros(max(n_ps, 1), dtype=np.float32)
+    for k in range(2, n_ps + 1):
+        co[k - 1] = (-1) ** (k + 1) / k * coeff_fn(k)
+    out = torch.empty(B, device=x.device)
+    ws = _hip.workspace(x.device, net.ws_bytes(B))
+    _hip.check(net.lib.inf_logdet_exact_trace(net.handle, _hip.ptr(x.contiguous()),
+                                              co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), max(n_ps, 1),
+                                              _hip.ptr(out), B, _hip.ptr(ws), ws.numel(), stream),
+               'inf_logdet_exact_trace')
+    return out
 
 
 def rademacher_probes(shape, device, mode='reference', seed=0, offset=0):

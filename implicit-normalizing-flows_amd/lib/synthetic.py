@@ -55,8 +55,11 @@ TOY = dict(
     geom_p=0.5, brute_force=True,
 )
 
+# POWER with exact_trace=True (implicit_block.py:323-343): a parity case for the exact-trace series.
+POWER_EXACT = dict(POWER, exact_trace=True)
+
 CONFIGS = {'cifar10': CIFAR10, 'cifar10_small': CIFAR10_SMALL, 'celebahq256': CELEBAHQ256,
-           'power': POWER, 'toy': TOY}
+           'power': POWER, 'toy': TOY, 'power_exact': POWER_EXACT}
 
 
 def _rng(seed, key):

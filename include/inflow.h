@@ -127,6 +127,11 @@ int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const f
                        float* out, int batch, void* ws, size_t ws_bytes, void* stream);
 /* Exact log|det(I + J_nnet(x))| for fc nets with d <= 16 (implicit_block.py:249-260,358-362). */
 int inf_logdet_exact(InfNet* net, const float* x, float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* Power series with the exact trace, exact_trace=True (implicit_block.py:323-343, iresblock.py:150-157):
+ * J = d nnet / dx by forward mode, out[b] = tr(J) + sum_{k=2..n} coeff[k-1] tr(J^k).  fc nets, d <= 16.
+ * coeff is a HOST array of n_terms values ((-1)^(k+1)/k coeff_fn(k); coeff[0] is ignored). */
+int inf_logdet_exact_trace(InfNet* net, const float* x, const float* coeff, int n_terms, float* out, int batch,
+                           void* ws, size_t ws_bytes, void* stream);
 
 /* ---- flow glue (elemwise.py:112-128, act_norm.py:153-193, squeeze.py:242-255,
  *      train_img.py:135-137,543-549) ---------------------------------------------------------- */

@@ -263,6 +263,11 @@ def neumann_logdet_estimator(g, x, n_power_series, vareps, coeff_fn):
     return torch.sum(vjp_jac.view(x.shape[0], -1) * vareps.view(x.shape[0], -1), 1)
 
 
+def batch_trace(M):
+    """implicit_block.py:364-365."""
+    return M.view(M.shape[0], -1)[:, ::M.shape[1] + 1].sum(1)
+
+
 def batch_jacobian(g, x):
     """implicit_block.py:358-362"""
     jac = []
@@ -299,6 +304,19 @@ class ImBlock:
             n_exact = a['n_exact_terms'] if self.training else a['n_exact_terms_test']
             n_ps, coeff_fn, ns = series_plan(a['n_dist'], self.lamb, self.geom_logit, n_exact)
             self.record['n_power_series'] = int(n_ps)
+            if a.get('exact_trace', False):          # implicit_block.py:323-343
+                x = x.detach().requires_grad_(True)
+                z = z.detach().requires_grad_(True)
+                out = []
+                for f, t in ((self.fx, x), (self.fz, z)):
+                    J = batch_jacobian(f(t), t)
+                    acc = batch_trace(J)
+                    Jk = J
+                    for k in range(2, n_ps + 1):
+                        Jk = torch.bmm(J, Jk)
+                        acc = acc + (-1) ** (k + 1) / k * coeff_fn(k) * batch_trace(Jk)
+                    out.append(acc)
+                return (out[0] - out[1]).view(-1, 1).detach()
             vareps_x = rademacher_like(x)
             vareps_z = rademacher_like(z)
             est = basic_logdet_estimator if estimator == 'basic' else neumann_logdet_estimator

@@ -118,7 +118,7 @@ def fc_model(arch):
         return torch.nn.Sequential(*nnet)
 
     blocks = [layers.imBlock(build_nnet(), build_nnet(), n_dist=arch['n_dist'], n_power_series=None,
-                             exact_trace=False, brute_force=arch['brute_force'], n_samples=1,
+                             exact_trace=arch.get('exact_trace', False), brute_force=arch['brute_force'], n_samples=1,
                              n_exact_terms=arch['n_exact_terms'], neumann_grad=False, grad_in_forward=False,
                              eps_forward=arch['eps_forward'])
               for _ in range(arch['n_blocks'])]
@@ -177,6 +177,8 @@ CASES = {
     'power_eval_b256': lambda: run_case('power_eval_b256', syn.POWER, syn.tabular_batch(256, 6, seed=3), seed=7),
     'power_train_b256': lambda: run_case('power_train_b256', syn.POWER, syn.tabular_batch(256, 6, seed=3),
                                          seed=7, train=True),
+    'power_exact_train_b64': lambda: run_case('power_exact_train_b64', syn.POWER_EXACT,
+                                              syn.tabular_batch(64, 6, seed=4), seed=9, train=True),
     'cifar_small_b4': lambda: run_case('cifar_small_b4', syn.CIFAR10_SMALL, syn.image_batch(4, seed=3), seed=7),
     'cifar_full_b2': lambda: run_case('cifar_full_b2', syn.CIFAR10, syn.image_batch(2, seed=3), seed=7),
     'cifar_full_b8': lambda: run_case('cifar_full_b8', syn.CIFAR10, syn.image_batch(8, seed=5), seed=11),

@@ -125,6 +125,7 @@ def _golden(golden_dir, name):
     ('cifar_full_b8', syn.CIFAR10, False),
     ('power_eval_b256', syn.POWER, False),
     ('power_train_b256', syn.POWER, True),
+    ('power_exact_train_b64', syn.POWER_EXACT, True),
     ('toy_eval_b64', syn.TOY, False),
 ])
 def test_flow_matches_reference_golden(golden_dir, name, arch, train):

@@ -13,6 +13,7 @@ CASES = [
     ('toy_eval_b64', syn.TOY, False),
     ('power_eval_b256', syn.POWER, False),
     ('power_train_b256', syn.POWER, True),
+    ('power_exact_train_b64', syn.POWER_EXACT, True),
     ('cifar_small_b4', syn.CIFAR10_SMALL, False),
     ('cifar_full_b2', syn.CIFAR10, False),
 ]
