@@ -27,7 +27,6 @@
 
 namespace inf {
 
-constexpr int F_BN_MAX = 64;      // pixels per tile (64, or 32 for small grids)
 // LDS per workgroup: 64-pixel tiles take the whole 160 KiB (one workgroup per CU); 32-pixel tiles
 // take 80 KiB so two workgroups share a CU and overlap each other's staging / epilogues / barriers.
 template <int F_BN>

@@ -18,6 +18,12 @@ LIB_PATH = os.path.join(_HERE, 'libinflow.so')
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 
 
+class PowerIterDesc(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int), ('cin', ctypes.c_int), ('cout', ctypes.c_int), ('ksize', ctypes.c_int),
+                ('height', ctypes.c_int), ('width', ctypes.c_int), ('weight', ctypes.c_void_p),
+                ('u', ctypes.c_void_p), ('v', ctypes.c_void_p), ('scale', ctypes.c_void_p)]
+
+
 class LayerDesc(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int), ('cin', ctypes.c_int), ('cout', ctypes.c_int), ('ksize', ctypes.c_int),
                 ('weight', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('u', ctypes.c_void_p),
@@ -88,6 +94,9 @@ _SIGS = {
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
+    'inf_power_iteration_workspace_bytes': (ctypes.c_size_t, [ctypes.POINTER(PowerIterDesc)]),
+    'inf_power_iteration': (ctypes.c_int, [ctypes.POINTER(PowerIterDesc), ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                           ctypes.c_float, ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),
 }
 EXPORTS = tuple(_SIGS)
 

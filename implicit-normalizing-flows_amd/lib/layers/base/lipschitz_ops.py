@@ -9,6 +9,7 @@ that scale and repacks the weights itself (``inf_net_refresh``); the methods her
 
 Only the domain = codomain = 2 (spectral) case that every run_*.sh config selects is provided.
 """
+import ctypes
 import math
 
 import torch
@@ -25,16 +26,36 @@ def _unit(t):
 
 def _power_iterate(apply_w, apply_wt, u, v, max_itrs, atol, rtol):
     """u <- W v / |.|, v <- W^T u / |.| until both move less than atol + rtol*max (mixed_lipschitz.py:295-310,348-368)."""
+    used = 0
     for _ in range(max_itrs):
         u_prev, v_prev = u, v
         u = _unit(apply_w(v))
         v = _unit(apply_wt(u))
+        used += 1
         if atol is not None and rtol is not None:
             du = torch.norm(u - u_prev) / (u.nelement() ** 0.5)
             dv = torch.norm(v - v_prev) / (v.nelement() ** 0.5)
             if du < atol + rtol * torch.max(u) and dv < atol + rtol * torch.max(v):
                 break
+    _power_iterate.last_used = used
     return u, v
+
+
+def _native_power_iteration(kind, cin, cout, ksize, hw, W, u, v, scale, itrs, atol, rtol, use_tol):
+    """inf_power_iteration: the whole loop on the engine, u / v / scale updated in place.  Returns the
+    iteration count.  The version counters are bumped so the engine's packed weights refresh."""
+    from ... import _hip
+    lib = _hip.load()
+    d = _hip.PowerIterDesc(kind=kind, cin=cin, cout=cout, ksize=ksize, height=hw[0], width=hw[1],
+                           weight=W.data_ptr(), u=u.data_ptr(), v=v.data_ptr(), scale=scale.data_ptr())
+    ws = _hip.workspace(W.device, lib.inf_power_iteration_workspace_bytes(ctypes.byref(d)))
+    used = ctypes.c_int(0)
+    _hip.check(lib.inf_power_iteration(ctypes.byref(d), int(itrs), int(bool(use_tol)), float(atol or 0.),
+                                       float(rtol or 0.), ctypes.byref(used), _hip.ptr(ws), ws.numel(),
+                                       _hip.stream_of(W)), 'inf_power_iteration')
+    for t in (u, v, scale):
+        torch.autograd.graph.increment_version(t)
+    return used.value
 
 
 def _iteration_budget(n_iterations, atol, rtol):
@@ -78,10 +99,18 @@ class InducedNormLinear(nn.Module):
             itrs = _iteration_budget(n_iterations, atol, rtol)
             with torch.no_grad():
                 tol = (atol, rtol) if n_iterations is None else (None, None)
-                u, v = _power_iterate(lambda t: torch.mv(W, t), lambda t: torch.mv(W.t(), t), self.u, self.v,
-                                      itrs, *tol)
-                self.u.copy_(u)
-                self.v.copy_(v)
+                if W.is_cuda:
+                    self.last_power_iters = _native_power_iteration(
+                        2, self.in_features, self.out_features, 1, (1, 1), W.detach(), self.u, self.v, self.scale,
+                        itrs, atol, rtol, n_iterations is None)
+                    if not torch.is_grad_enabled():
+                        return W / torch.clamp(self.scale / self.coeff, min=1.)
+                else:       # construction-time init on the host (the module is built on CPU, then moved)
+                    u, v = _power_iterate(lambda t: torch.mv(W, t), lambda t: torch.mv(W.t(), t), self.u, self.v,
+                                          itrs, *tol)
+                    self.u.copy_(u)
+                    self.v.copy_(v)
+                    self.last_power_iters = _power_iterate.last_used
         sigma = torch.dot(self.u, torch.mv(W, self.v))
         with torch.no_grad():
             self.scale.copy_(sigma)
@@ -183,9 +212,21 @@ class InducedNormConv2d(nn.Module):
         if update:
             with torch.no_grad():
                 tol = (atol, rtol) if n_iterations is None else (None, None)
-                u, v = _power_iterate(fwd, bwd, self.u.view(-1), self.v.view(-1), itrs, *tol)
-                self.u.copy_(u.view_as(self.u))
-                self.v.copy_(v.view_as(self.v))
+                if W.is_cuda:
+                    k = self.kernel_size[0]
+                    if self.kernel_size != (k, k) or self.stride != (1, 1) or self.padding != (k // 2, k // 2):
+                        raise NotImplementedError('engine power iteration: square kernels, stride 1, padding k//2')
+                    hw = (1, 1) if self.is_1x1 else self._hw()
+                    self.last_power_iters = _native_power_iteration(
+                        1, self.in_channels, self.out_channels, self.kernel_size[0], hw, W.detach(), self.u,
+                        self.v, self.scale, itrs, atol, rtol, n_iterations is None)
+                    if not torch.is_grad_enabled():
+                        return W / torch.clamp(self.scale / self.coeff, min=1.)
+                else:       # construction-time init on the host (the module is built on CPU, then moved)
+                    u, v = _power_iterate(fwd, bwd, self.u.view(-1), self.v.view(-1), itrs, *tol)
+                    self.u.copy_(u.view_as(self.u))
+                    self.v.copy_(v.view_as(self.v))
+                    self.last_power_iters = _power_iterate.last_used
         sigma = torch.dot(self.u.view(-1), fwd(self.v))
         with torch.no_grad():
             self.scale.copy_(sigma)

@@ -160,6 +160,24 @@ typedef struct InfKernelStat {
 int inf_profile_begin(int max_launches);
 int inf_profile_end(InfKernelStat* out, int max_out, int* n_out);
 
+/* ---- Lipschitz power iteration: compute_weight(update=True) of InducedNormConv2d / InducedNormLinear,
+ *      spectral (2 -> 2) case (mixed_lipschitz.py:85-124 linear, :276-326 1x1 conv, :328-386 k x k conv;
+ *      called by update_lipschitz, train_img.py:786-792) -------------------------------------------- */
+typedef struct InfPowerIterDesc {
+  int kind;              /* INF_LAYER_CONV or INF_LAYER_LINEAR */
+  int cin, cout, ksize;  /* conv: stride 1, padding ksize/2; linear: ksize ignored */
+  int height, width;     /* k x k conv: spatial_dims, the (H, W) that u (cout*H*W) and v (cin*H*W) live on */
+  const float* weight;   /* raw weight (cout, cin, k, k) / (cout, cin) */
+  float* u;              /* module buffers, updated in place (u <- W v / |W v|, v <- W^T u / |W^T u|) */
+  float* v;
+  float* scale;          /* receives sigma = u . (W v) (the module's `scale` buffer); may be NULL */
+} InfPowerIterDesc;
+size_t inf_power_iteration_workspace_bytes(const InfPowerIterDesc* desc);
+/* Up to max_iters iterations; with use_tol, stop once |du|/sqrt(n_u) < atol + rtol max(u) and the same for
+ * v.  iters_used (may be NULL) receives the count. */
+int inf_power_iteration(const InfPowerIterDesc* desc, int max_iters, int use_tol, float atol, float rtol,
+                        int* iters_used, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);

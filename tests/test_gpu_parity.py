@@ -6,6 +6,7 @@ Tolerances (north star: bits/dim within 1e-5 abs of the reference):
   * per-sample log p(x):              |delta| <= 2e-3 nats   (=> <= 1e-6 bpd per sample at d=3072)
   * net forward / VJP / z:            |delta| <= 2e-5 * max(1, |ref|_inf)  (fp32, reordered sums)
 """
+import copy
 import ctypes
 import os
 
@@ -280,3 +281,37 @@ def test_fused_313_matches_generic_path(block, B, monkeypatch):
         assert torch.isfinite(a).all()
     for a, b in zip(outs['fused'], outs['generic']):
         _close(a, b, rel=1e-5)
+
+
+@pytest.mark.parametrize('kind', ['conv3', 'conv1', 'linear', 'conv3_fixed', 'conv3_cifar'])
+def test_power_iteration_matches_host(kind):
+    """compute_weight(update=True) on the engine (power.hip) vs the host restatement of
+    mixed_lipschitz.py:85-124,276-386 on the same starting u, v: same iteration count, u, v, sigma."""
+    from lib.layers.base import lipschitz_ops as lo
+    torch.manual_seed(5)
+    if kind == 'linear':
+        m = lo.InducedNormLinear(128, 96, coeff=0.99, atol=1e-3, rtol=1e-3)
+    elif kind == 'conv3_cifar':                        # last conv of a run_cifar10.sh net at s0
+        m = lo.InducedNormConv2d(512, 3, 3, 1, 1, coeff=0.9, atol=1e-3, rtol=1e-3)
+        with torch.no_grad():
+            m(torch.zeros(1, 512, 32, 32))
+    else:
+        k = 1 if kind == 'conv1' else 3
+        m = lo.InducedNormConv2d(12, 64, k, 1, k // 2, coeff=0.9, atol=1e-3, rtol=1e-3)
+        with torch.no_grad():
+            m(torch.zeros(1, 12, 16, 16))             # lazy u/v on the host (spatial dims 16x16)
+    with torch.no_grad():
+        m.weight.add_(0.05 * torch.randn_like(m.weight))   # move away from the converged u, v
+    host = copy.deepcopy(m)
+    dev = copy.deepcopy(m).to(DEV)
+    n_it = 7 if kind == 'conv3_fixed' else None
+    with torch.no_grad():
+        host.compute_weight(update=True, n_iterations=n_it)
+        w_dev = dev.compute_weight(update=True, n_iterations=n_it)
+    torch.cuda.synchronize()
+    assert dev.last_power_iters == host.last_power_iters
+    np.testing.assert_allclose(dev.u.cpu().numpy(), host.u.numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_allclose(dev.v.cpu().numpy(), host.v.numpy(), rtol=0, atol=1e-5)
+    assert abs(dev.scale.item() - host.scale.item()) <= 1e-5 * abs(host.scale.item())
+    w_host = host.compute_weight(update=False)
+    np.testing.assert_allclose(w_dev.cpu().numpy(), w_host.detach().numpy(), rtol=1e-5, atol=1e-7)
