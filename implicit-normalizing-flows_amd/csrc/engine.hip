@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <new>
+#include <functional>
 #include <vector>
 
 #include "glue.h"
@@ -341,6 +342,18 @@ int run_vjp(InfNet* n, const float* v, float* vout, const float* xin, const floa
   return n->fc ? launch_fc_out(a, B, s) : launch_conv_out(a, B, s);
 }
 
+// per-sample sums of squares (partials in bf.part) -> host (the reference's .item() per iteration)
+int read_sumsq(InfNet* f, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+  if (f->fc) {
+    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  } else {
+    INF_TRY(launch_reduce_partials(bf.part, B, bf.nchunk, bf.sumsq, s));
+    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  }
+  INF_HIP(hipStreamSynchronize(s));
+  return INF_OK;
+}
+
 // residual evaluation g = x_embed - f(z) - z (+ dg = g - g_prev) and per-sample sum of squares -> host
 // zsub is the subtracted "- z" term: z itself for Broyden, zeros for the Banach map x_embed - f(z).
 int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
@@ -355,13 +368,15 @@ int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, 
   a.partial = bf.part;
   a.nchunk = bf.nchunk;
   INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
-  if (f->fc) {
-    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-  } else {
-    INF_TRY(launch_reduce_partials(bf.part, B, bf.nchunk, bf.sumsq, s));
-    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-  }
-  INF_HIP(hipStreamSynchronize(s));
+  return read_sumsq(f, B, bf, host_sumsq, s);
+}
+
+// vjp residual of the implicit backward (implicit_block.py:186-190): g = (y + y^T J) - grad
+int vjp_resid(InfNet* f, const float* y, const float* zi, const float* gradi, float* gout, float* dg,
+              const float* gprev, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+  INF_TRY(run_vjp(f, y, bf.tmp, zi, nullptr, nullptr, B, bf, s));
+  INF_TRY(launch_vjp_resid(bf.tmp, y, gradi, gprev, gout, dg, bf.part, B, f->d, f->fc ? 1 : bf.nchunk, f->fc, s));
+  return read_sumsq(f, B, bf, host_sumsq, s);
   return INF_OK;
 }
 
@@ -391,14 +406,19 @@ bool same_shape(const InfNet* a, const InfNet* b) {
 
 // Broyden root find on internal-layout buffers.  Solves z with g(z) = xemb - f(z) - z = 0.
 // Result (lowest iterate) in bf.lowest.  y (internal) is the Banach fallback start.
-int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
-                  Bufs& bf, hipStream_t s) {
+// residual g(x) -> gout (+ dg = g - gprev when gprev), per-sample sums of squares -> host
+using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev,
+                                  std::vector<double>& host_sumsq)>;
+
+// broyden.py:123-193 with the residual as a callback; the result (lowest iterate) is in bf.lowest.
+int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
+                 std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
-  std::vector<double> ss(B), lowest_ss(B);
+  std::vector<double> ss(B);
+  lowest_ss.assign(B, 0.0);
   const double eps = eps_in * sqrt((double)E);                       // broyden.py:131
-  InfBroydenStats stats;
   memset(&stats, 0, sizeof(stats));
   stats.eps = eps;
 
@@ -406,7 +426,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
   INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
-  INF_TRY(eval_resid(f, x, x, bf.xemb, gx, nullptr, nullptr, B, bf, ss, s));
+  INF_TRY(resid(x, gx, nullptr, nullptr, ss));
   const double init = sqrt(total(ss));
   double obj = init, lowest = init;
   lowest_ss = ss;
@@ -417,7 +437,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
   INF_TRY(launch_axpy_step(x, bf.upd, xn, bf.dx, (long)E, s));
   while (obj >= eps && nstep < T) {                                   // broyden.py:153
-    INF_TRY(eval_resid(f, xn, xn, bf.xemb, gn, bf.dg, gx, B, bf, ss, s));
+    INF_TRY(resid(xn, gn, bf.dg, gx, ss));
     std::swap(x, xn);
     std::swap(gx, gn);
     nstep += 1;
@@ -470,6 +490,18 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   stats.diff = lowest;
   stats.n_trace = (int)std::min<size_t>(trace.size(), 64);
   for (int k = 0; k < stats.n_trace; ++k) stats.trace[k] = trace[k];
+  return INF_OK;
+}
+
+int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
+                  Bufs& bf, hipStream_t s) {
+  const size_t E = (size_t)B * f->d;
+  InfBroydenStats stats;
+  std::vector<double> lowest_ss;
+  const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
+    return eval_resid(f, x, x, bf.xemb, gout, dg, gprev, B, bf, ss, s);
+  };
+  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s));
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -787,6 +819,48 @@ int inf_imblock_forward(InfNet* nx, InfNet* nz, const float* x, float* z, int B,
   return INF_OK;
 }
 
+// Implicit backward of an imBlock (imBlock.Backward.backward, implicit_block.py:176-217):
+//   dl_dh: Broyden root of g(y) = y (I + J_fz(z)) - grad from y = 0 (eps_backward, threshold), lowest iterate;
+//   dl_dx = dl_dh (I + J_fx(x)).
+int inf_imblock_backward(InfNet* nx, InfNet* nz, const float* z, const float* x, const float* grad, float* dl_dh,
+                         float* dl_dx, int B, int T, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes,
+                         void* stream) {
+  if (!nx || !nz || !z || !x || !grad || !dl_dh || !dl_dx || B <= 0 || T <= 0 || T > 64 || !same_shape(nx, nz))
+    return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  {
+    Bufs bf;
+    if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+    int st = INF_OK;
+    const float* zi = to_internal(nz, z, bf.xin, B, s, &st);
+    INF_TRY(st);
+    const float* gi = to_internal(nz, grad, bf.xemb, B, s, &st);
+    INF_TRY(st);
+    INF_TRY(run_forward(nz, zi, B, bf, -1, nullptr, s));      // activation derivatives at z
+    InfBroydenStats bs;
+    std::vector<double> lowest_ss;
+    const ResidFn resid = [&](const float* y, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
+      return vjp_resid(nz, y, zi, gi, gout, dg, gprev, B, bf, ss, s);
+    };
+    INF_TRY(broyden_core(nz, resid, B, T, eps, bs, lowest_ss, bf, s));
+    if (stats) *stats = bs;
+    INF_TRY(to_boundary(nz, bf.lowest, dl_dh, B, s));
+  }
+  // dl_dx = dl_dh + dl_dh^T J_fx(x)   (Fx = nnet_x(x) + x; Fx.backward(dl_dh), :210-213)
+  Bufs bf;
+  if (carve(nx, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(nx, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* hi = to_internal(nx, dl_dh, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(run_forward(nx, xi, B, bf, -1, nullptr, s));
+  INF_TRY(run_vjp(nx, hi, bf.va, xi, nullptr, nullptr, B, bf, s));
+  INF_TRY(glue_add(bf.va, hi, nx->fc ? bf.tmp : dl_dx, (long)B * nx->d, s));
+  if (nx->fc) INF_TRY(to_boundary(nx, bf.tmp, dl_dx, B, s));
+  return INF_OK;
+}
+
 // Power series of 1 or 2 fused nets of the same shape (the x- and z-branch of an imBlock advance in
 // lockstep: one launch per term over both nets' tiles).  Term k's VJP stages term k-1's packed taps
 // directly (tap sum, preact swish', trace partial -- conv_out's work), so a term is ONE launch; only
@@ -903,20 +977,12 @@ int inf_logdet_series_pair(InfNet* na, const float* xa, const float* ea, InfNet*
   return series_fused(nets, xs, es, 2, coeff, n_terms, outs, B, bfs, s);
 }
 
-int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,
-                       int B, void* ws, size_t ws_bytes, void* stream) {
-  if (!n || !x || !vareps || !ncoeff || !out || B <= 0 || n_terms < 0) return INF_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream;
-  Bufs bf;
-  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+// neumann_vjp of neumann_logdet_estimator (implicit_block.py:429-436): w = eps + sum_k ncoeff[k] eps^T J^k,
+// accumulated in k order into bf.tmp (internal layout).  Leaves the activation derivatives of x saved.
+static int neumann_w(InfNet* n, const float* xi, const float* ei, const float* ncoeff, int n_terms, int B, Bufs& bf,
+                     hipStream_t s) {
   const size_t E = (size_t)B * n->d;
-  int st = INF_OK;
-  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
-  INF_TRY(st);
-  const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
-  INF_TRY(st);
   INF_TRY(run_forward(n, xi, B, bf, -1, nullptr, s));
-  // neumann_vjp = vareps ; vjp = vareps
   INF_HIP(hipMemcpyAsync(bf.tmp, ei, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
   const float* v = ei;
   for (int k = 1; k <= n_terms; ++k) {
@@ -925,6 +991,36 @@ int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const flo
     INF_TRY(glue_axpy_scaled(bf.tmp, vo, ncoeff[k], (long)E, s));
     v = vo;
   }
+  return INF_OK;
+}
+
+int inf_neumann_vector(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* w,
+                       int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !vareps || !ncoeff || !w || B <= 0 || n_terms < 0) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(neumann_w(n, xi, ei, ncoeff, n_terms, B, bf, s));
+  return to_boundary(n, bf.tmp, w, B, s);
+}
+
+int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,
+                       int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !vareps || !ncoeff || !out || B <= 0 || n_terms < 0) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  const float* ei = to_internal(n, vareps, bf.eps_t, B, s, &st);
+  INF_TRY(st);
+  INF_TRY(neumann_w(n, xi, ei, ncoeff, n_terms, B, bf, s));
   INF_TRY(run_vjp(n, bf.tmp, bf.va, xi, ei, bf.part, B, bf, s));
   const float one = 1.f;
   return launch_series_combine(bf.part, &one, 1, B, bf.nchunk, out, s);

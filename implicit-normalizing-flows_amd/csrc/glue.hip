@@ -164,6 +164,17 @@ int glue_init_tangents(const float* xT, float* ext, int d, int B, hipStream_t s)
   return INF_OK;
 }
 
+__global__ void add_kernel(const float* a, const float* b, float* out, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = b[i] + a[i];
+}
+// out = b + a  (x.grad accumulation order of Fx.backward: the identity branch, then the net branch)
+int glue_add(const float* a, const float* b, float* out, long n, hipStream_t s) {
+  hipLaunchKernelGGL(add_kernel, GRID1(n), 0, s, a, b, out, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // 160 KiB of LDS per workgroup, one workgroup per CU at a time; 8 waves of 4 per CU cover every CU.
 __global__ __launch_bounds__(1024) void poison_lds_kernel(float* sink) {
   __shared__ float lds[40960];

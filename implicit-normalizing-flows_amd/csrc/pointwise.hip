@@ -100,6 +100,55 @@ int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
   return INF_OK;
 }
 
+// Implicit-backward residual (implicit_block.py:186-190): g = (y + v) - grad with v = y^T J (the VJP),
+// dg = g - gprev (gprev may be null), per-sample partial sums of g^2.
+// Conv layout (B, d): grid (nchunk, B), partial[b * nchunk + chunk].  fc layout (d, B): one thread per
+// sample, partial[b].
+__global__ __launch_bounds__(256) void vjp_resid_kernel(const float* v, const float* y, const float* grad,
+                                                        const float* gprev, float* g, float* dg, double* partial,
+                                                        int d, int nchunk) {
+  __shared__ double red[16];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const long base = (long)b * d;
+  const int lo = chunk * OUT_CH, hi = min(d, lo + OUT_CH);
+  double acc = 0.0;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const long e = base + i;
+    const float gv = (y[e] + v[e]) - grad[e];
+    g[e] = gv;
+    if (gprev) dg[e] = gv - gprev[e];
+    acc += (double)gv * (double)gv;
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[(long)b * nchunk + chunk] = t;
+}
+__global__ void vjp_resid_fc_kernel(const float* v, const float* y, const float* grad, const float* gprev, float* g,
+                                    float* dg, double* partial, int d, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double acc = 0.0;
+  for (int j = 0; j < d; ++j) {
+    const long e = (long)j * batch + b;
+    const float gv = (y[e] + v[e]) - grad[e];
+    g[e] = gv;
+    if (gprev) dg[e] = gv - gprev[e];
+    acc += (double)gv * (double)gv;
+  }
+  partial[b] = acc;
+}
+int launch_vjp_resid(const float* v, const float* y, const float* grad, const float* gprev, float* g, float* dg,
+                     double* partial, int batch, int d, int nchunk, int fc, hipStream_t s) {
+  if (fc) {
+    hipLaunchKernelGGL(vjp_resid_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, v, y, grad, gprev, g, dg,
+                       partial, d, batch);
+  } else {
+    hipLaunchKernelGGL(vjp_resid_kernel, dim3(out_nchunk(d), batch), dim3(256), 0, s, v, y, grad, gprev, g, dg,
+                       partial, d, nchunk);
+  }
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // fc nets: tensors are feature-major (d, B); Y rows are (d, B); one thread per sample.
 __global__ __launch_bounds__(256) void fc_out_kernel(OutArgs a, int batch) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;

@@ -72,6 +72,8 @@ _SIGS = {
     'inf_net_vjp': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_root_find': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                      ctypes.POINTER(BroydenStats), _P, _P, ctypes.c_size_t, _P]),
+    'inf_imblock_backward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                            ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_imblock_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                            ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_broyden_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -82,6 +84,8 @@ _SIGS = {
     'inf_logdet_series_pair': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                               _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_neumann': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
+                                          ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_neumann_vector': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                           ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact_trace': (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, ctypes.c_int,

@@ -46,3 +46,22 @@ def tabular_logpx(model, x):
 def bits_per_dim_from_sum(sum_logpx, count, ndim):
     """bpd of a (possibly sharded) batch from the all-reduced [sum logpx, N]."""
     return -(sum_logpx / count) / ndim / math.log(2)
+
+
+def image_bits_per_dim_graph(model, x, nvals=256):
+    """compute_loss with gradients (train_img.py:517-554, density task, padding 0, beta 1):
+    returns (bits_per_dim, logpx (B, 1), z) connected to the model's parameters."""
+    z, delta_logp = model(x, 0)
+    logpz = (-0.5 * math.log(2 * math.pi) - z.pow(2) / 2).view(z.size(0), -1).sum(1, keepdim=True)
+    ndim = x[0].numel()
+    logpu = torch.zeros(x.shape[0], 1, device=x.device)          # add_padding with padding 0
+    logpx = logpz - delta_logp - np.log(nvals) * ndim - logpu
+    return -torch.mean(logpx) / ndim / np.log(2), logpx, z
+
+
+def tabular_nats_graph(model, x):
+    """train_tabular.py:398-410 with gradients: (-mean log p(x) in nats, logpx, z)."""
+    z, delta_logp = model(x, torch.zeros(x.shape[0], 1, device=x.device))
+    logpz = (-0.5 * math.log(2 * math.pi) - z.pow(2) / 2).view(z.size(0), -1).sum(1, keepdim=True)
+    logpx = logpz - delta_logp
+    return -torch.mean(logpx), logpx, z

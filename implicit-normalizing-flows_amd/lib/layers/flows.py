@@ -63,9 +63,14 @@ class Inverse(nn.Module):
         return self.flow.forward(y, logpy)
 
 
+def _graph(*ts):
+    """A gradient must flow through this op: take the differentiable torch expression."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
 def squeeze(x, downscale_factor=2):
     """[B, C, H*r, W*r] -> [B, C*r^2, H, W] (squeeze.py:242-255)."""
-    if downscale_factor == 2 and x.is_cuda and x.dtype == torch.float32:
+    if downscale_factor == 2 and x.is_cuda and x.dtype == torch.float32 and not _graph(x):
         B, C, H, W = x.shape
         x = x.contiguous()
         y = torch.empty(B, 4 * C, H // 2, W // 2, device=x.device)
@@ -127,7 +132,8 @@ class _ActNorm(nn.Module):
             self.__dict__['_init_seen'] = True
         B, C = x.shape[0], x.shape[1]
         hw = x[0, 0].numel()
-        if x.is_cuda and x.dtype == torch.float32:
+        lgraph = logpx if torch.is_tensor(logpx) else None
+        if x.is_cuda and x.dtype == torch.float32 and not _graph(x, self.weight, self.bias, lgraph):
             x = x.contiguous()
             y = torch.empty_like(x)
             lin = _logp_tensor(logpx, B, x.device)
@@ -169,7 +175,8 @@ class LogitTransform(nn.Module):
 
     def forward(self, x, logpx=None, restore=False):
         B = x.shape[0]
-        if x.is_cuda and x.dtype == torch.float32:
+        lgraph = logpx if torch.is_tensor(logpx) else None
+        if x.is_cuda and x.dtype == torch.float32 and not _graph(x, lgraph):
             x = x.contiguous()
             y = torch.empty_like(x)
             lin = _logp_tensor(logpx, B, x.device)

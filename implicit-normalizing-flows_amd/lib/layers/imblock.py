@@ -16,8 +16,10 @@ RNG) and, in the default ``'reference'`` probe mode, the Rademacher probes from 
 generator in the reference's order (vareps_x, then vareps_z), so seeded runs replay exactly.
 ``set_probe_mode('device')`` draws the probes on the GPU instead (counter-based generator).
 
-Training (implicit backward, mem-efficient estimator gradients) is not implemented yet; a
-train-mode forward that needs gradients raises instead of returning a graph-less value.
+When a gradient is needed (training), the forward builds the reference's graph: the root solve and
+the n-term Neumann series run on the engine, the implicit backward (imBlock.Backward) is an engine
+Broyden solve over VJPs (inf_imblock_backward), and the once-per-step parameter-gradient
+bookkeeping (recompute graph, the surrogate's double backward) goes through autograd on the nets.
 """
 import copy
 import ctypes
@@ -45,6 +47,67 @@ def _probes(shape, device):
     out = solvers.rademacher_probes(shape, device, _PROBES['mode'], _PROBES['seed'], _PROBES['offset'])
     _PROBES['offset'] += int(np.prod(shape))
     return out
+
+
+class _ImplicitBackward(torch.autograd.Function):
+    """imBlock.Backward (implicit_block.py:165-217): identity in the forward pass; the backward pass
+    solves dl_dh (I + J_fz(z)) = grad by Broyden on the engine (inf_imblock_backward) and returns
+    dl_dh into z's recompute graph and dl_dx = dl_dh (I + J_fx(x)) into x."""
+
+    @staticmethod
+    def forward(ctx, z, x, blk):
+        ctx.save_for_backward(z.detach(), x.detach())
+        ctx.blk = blk
+        return z.clone()
+
+    @staticmethod
+    def backward(ctx, grad):
+        z, x = ctx.saved_tensors
+        blk = ctx.blk
+        nx, nz, stream = blk._native(x)
+        B, T = x.shape[0], int(blk.threshold)
+        ws = _hip.workspace(x.device, max(nz.ws_bytes(B, T), nx.ws_bytes(B, 1)))
+        grad = grad.contiguous()
+        dl_dh, dl_dx = torch.empty_like(grad), torch.empty_like(grad)
+        st = _hip.BroydenStats()
+        _hip.check(_hip.load().inf_imblock_backward(nx.handle, nz.handle, _hip.ptr(z.contiguous()),
+                                                    _hip.ptr(x.contiguous()), _hip.ptr(grad), _hip.ptr(dl_dh),
+                                                    _hip.ptr(dl_dx), B, T, float(blk.eps_backward), ctypes.byref(st),
+                                                    _hip.ptr(ws), ws.numel(), stream), 'inf_imblock_backward')
+        blk.last_broyden_backward = st.as_dict(T)
+        return dl_dh, dl_dx, None
+
+
+class _MemEffLogDet(torch.autograd.Function):
+    """MemoryEfficientLogDetEstimator (implicit_block.py:373-415): the estimator and its gradients with
+    respect to x and the net's parameters are computed in the forward pass; backward scales them by
+    the first element of the incoming gradient (the reference's dL = grad_logdetgrad[0])."""
+
+    @staticmethod
+    def forward(ctx, estimator, x, *params):
+        with torch.enable_grad():
+            xg = x.detach().requires_grad_(True)
+            ld = estimator(xg)
+            grad_x, *grad_params = torch.autograd.grad(ld.sum(), (xg,) + params, allow_unused=True)
+        if grad_x is None:
+            grad_x = torch.zeros_like(x)
+        ctx.n_params = len(params)
+        ctx.none_mask = [g is None for g in grad_params]
+        ctx.save_for_backward(grad_x, *[g for g in grad_params if g is not None])
+        return ld.detach()
+
+    @staticmethod
+    def backward(ctx, grad_ld):
+        grad_x, *saved = ctx.saved_tensors
+        dL = grad_ld[0].detach()
+        it = iter(saved)
+        grads = [None if none else next(it) * dL for none in ctx.none_mask]
+        return (None, grad_x * dL) + tuple(grads)
+
+
+def _needs_graph(module, *ts):
+    return torch.is_grad_enabled() and (any(t.requires_grad for t in ts) or
+                                        any(p.requires_grad for p in module.parameters()))
 
 
 def _uninitialised_convs(net):
@@ -104,12 +167,88 @@ class imBlock(nn.Module):
             nets.append(n)
         return nets[0], nets[1], stream
 
-    def _check_grad(self, *ts):
-        if self.training and torch.is_grad_enabled() and (
-                any(t.requires_grad for t in ts) or any(p.requires_grad for p in self.parameters())):
-            raise NotImplementedError('imBlock training backward (implicit_block.py:165-217, :373-415) is not '
-                                      'implemented on the MI355X engine yet; run train-mode forwards under '
-                                      'torch.no_grad()')
+    # ---------------------------------------------------------------------------------------
+    # Differentiable (training) path: implicit_block.py:220-234 with autograd
+    # ---------------------------------------------------------------------------------------
+    def _forward_graph(self, x, logpx, restore):
+        """z* by the engine's Broyden solve; z = f_x(x0) - f_z(z*) + x0 as a graph into the nets'
+        parameters (x0 = x detached, :226-227); the implicit backward (_ImplicitBackward) carries the
+        gradient into x; the log-det with gradients (_logdetgrad_graph)."""
+        if restore:
+            with torch.no_grad():
+                self.nnet_x_copy(x)
+                self.nnet_z_copy(x)
+        x0 = x.detach()
+        nx, nz, stream = self._native(x0)
+        with torch.no_grad():
+            z_star = self._root(nz, nx, x0, self.eps_forward, stream, forward=False)
+        z = (self.nnet_x(x0) - self.nnet_z(z_star)) + x0
+        if self.training:
+            self.nnet_x_copy.load_state_dict(self.nnet_x.state_dict())
+            self.nnet_z_copy.load_state_dict(self.nnet_z.state_dict())
+        z = _ImplicitBackward.apply(z, x, self)
+        if logpx is None:
+            return z
+        return z, logpx - self._logdetgrad_graph(z, x)
+
+    def _logdetgrad_graph(self, z, x):
+        """_logdetgrad with gradients (implicit_block.py:245-350).  The n-term Neumann series runs on the
+        engine (inf_neumann_vector); the surrogate w^T J eps and its parameter gradients go through
+        autograd on the nets."""
+        if (self.brute_force or not self.training) and x.dim() == 2 and x.shape[1] <= 10:
+            xg = x if x.requires_grad else x.detach().requires_grad_(True)
+            zg = z if z.requires_grad else z.detach().requires_grad_(True)
+            with torch.enable_grad():
+                Jx = solvers.batch_jacobian(xg + self.nnet_x(xg), xg)
+                Jz = solvers.batch_jacobian(zg + self.nnet_z(zg), zg)
+                return (torch.logdet(Jx) - torch.logdet(Jz)).view(-1, 1)
+        n_ps, coeff_fn, ns = self._series_plan()
+        if self.exact_trace:
+            with torch.enable_grad():
+                out = []
+                for net, t in ((self.nnet_x, x), (self.nnet_z, z)):
+                    tg = t if t.requires_grad else t.detach().requires_grad_(True)
+                    J = solvers.batch_jacobian(net(tg), tg)
+                    acc = solvers.batch_trace(J)
+                    Jk = J
+                    for k in range(2, n_ps + 1):
+                        Jk = torch.bmm(J, Jk)
+                        acc = acc + (-1) ** (k + 1) / k * coeff_fn(k) * solvers.batch_trace(Jk)
+                    out.append(acc)
+            return self._finish_logdet(out[0] - out[1], n_ps, ns)
+        vareps_x = _probes(x.shape, x.device)
+        vareps_z = _probes(z.shape, z.device)
+        neumann = self.training and self.neumann_grad
+        nx, nz, stream = self._native(x)
+        ests = []
+        for net, native, t, eps in ((self.nnet_x, nx, x, vareps_x), (self.nnet_z, nz, z, vareps_z)):
+            if neumann:
+                w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
+                est = (lambda net_, w_, eps_: lambda tg: solvers.surrogate_wJe(net_, tg, w_, eps_))(net, w, eps)
+            else:
+                est = (lambda net_, eps_: lambda tg: solvers.basic_series_graph(net_, tg, n_ps, eps_, coeff_fn,
+                                                                                self.training))(net, eps)
+            if self.training and self.grad_in_forward:
+                ests.append(_MemEffLogDet.apply(est, t, *list(net.parameters())))
+            else:
+                tg = t if t.requires_grad else t.detach().requires_grad_(True)
+                with torch.enable_grad():
+                    ests.append(est(tg))
+        return self._finish_logdet(ests[0] - ests[1], n_ps, ns)
+
+    def _neumann_vector(self, native, t, eps, n_ps, coeff_fn, stream):
+        B = t.shape[0]
+        nco = np.zeros(n_ps + 1, dtype=np.float32)
+        nco[0] = 1.
+        for k in range(1, n_ps + 1):
+            nco[k] = (-1) ** k * coeff_fn(k)
+        w = torch.empty_like(t)
+        ws = _hip.workspace(t.device, native.ws_bytes(B))
+        _hip.check(_hip.load().inf_neumann_vector(native.handle, _hip.ptr(t.contiguous()), _hip.ptr(eps),
+                                                  nco.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps,
+                                                  _hip.ptr(w), B, _hip.ptr(ws), ws.numel(), stream),
+                   'inf_neumann_vector')
+        return w
 
     def _root(self, net_f, net_e, y, eps, stream, forward):
         lib = _hip.load()
@@ -132,7 +271,8 @@ class imBlock(nn.Module):
 
     # ---------------------------------------------------------------------------------------
     def forward(self, x, logpx=None, restore=False):
-        self._check_grad(x)
+        if _needs_graph(self, x):
+            return self._forward_graph(x, logpx, restore)
         if restore:
             with torch.no_grad():
                 self.nnet_x_copy(x)
@@ -148,7 +288,6 @@ class imBlock(nn.Module):
         return z, logpx - self._logdetgrad(z, x)
 
     def inverse(self, z, logpy=None):
-        self._check_grad(z)
         nx, nz, stream = self._native(z)
         with torch.no_grad():
             x = self._root(nx, nz, z, self.eps_sample, stream, forward=False)

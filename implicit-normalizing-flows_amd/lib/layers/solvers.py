@@ -204,3 +204,17 @@ def batch_jacobian(g, x, create_graph=True):
 
 def batch_trace(M):
     return M.view(M.shape[0], -1)[:, ::M.shape[1] + 1].sum(1)
+
+
+def surrogate_wJe(net, x, w, vareps):
+    """The differentiable tail of neumann_logdet_estimator (implicit_block.py:437-438) for a Neumann
+    vector w computed by the engine: sum((w^T J) * vareps) per sample, with the graph kept so the
+    caller can differentiate it with respect to x and the net's parameters."""
+    g = net(x)
+    vjp_jac = torch.autograd.grad(g, x, w, create_graph=True)[0]
+    return torch.sum(vjp_jac.view(x.shape[0], -1) * vareps.view(x.shape[0], -1), 1)
+
+
+def basic_series_graph(net, x, n_power_series, vareps, coeff_fn, training):
+    """basic_logdet_estimator with the graph (training with neumann_grad=False, e.g. train_tabular.py)."""
+    return basic_logdet_estimator(net(x), x, n_power_series, vareps, coeff_fn, training)

@@ -125,8 +125,19 @@ int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_
  * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
 int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,
                        float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* The Neumann vector itself, w = vareps + sum_{k=1..n} ncoeff[k] vareps^T J^k (neumann_vjp,
+ * implicit_block.py:430-436), for the training surrogate's gradient. */
+int inf_neumann_vector(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* w,
+                       int batch, void* ws, size_t ws_bytes, void* stream);
 /* Exact log|det(I + J_nnet(x))| for fc nets with d <= 16 (implicit_block.py:249-260,358-362). */
 int inf_logdet_exact(InfNet* net, const float* x, float* out, int batch, void* ws, size_t ws_bytes, void* stream);
+/* Implicit backward of an imBlock (imBlock.Backward, implicit_block.py:165-217): given dL/dz = grad, solve
+ * dl_dh (I + J_fz(z)) = grad by Broyden from 0 (eps = eps_backward, threshold; lowest iterate), then
+ * dl_dx = dl_dh (I + J_fx(x)).  dl_dh is the gradient into z's recompute graph, dl_dx into x.
+ * ws >= max(inf_workspace_bytes(net_z, batch, threshold), inf_workspace_bytes(net_x, batch, 1)). */
+int inf_imblock_backward(InfNet* net_x, InfNet* net_z, const float* z, const float* x, const float* grad,
+                         float* dl_dh, float* dl_dx, int batch, int threshold, double eps, InfBroydenStats* stats,
+                         void* ws, size_t ws_bytes, void* stream);
 /* Power series with the exact trace, exact_trace=True (implicit_block.py:323-343, iresblock.py:150-157):
  * J = d nnet / dx by forward mode, out[b] = tr(J) + sum_{k=2..n} coeff[k-1] tr(J^k).  fc nets, d <= 16.
  * coeff is a HOST array of n_terms values ((-1)^(k+1)/k coeff_fn(k); coeff[0] is ignored). */
