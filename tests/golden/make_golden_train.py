@@ -102,7 +102,36 @@ def run_train_case(name, arch, x, seed, weight_seed=0):
         os.path.getsize(path) // 1024))
 
 
+def run_ires_case(name, neumann, mem_eff, B=64, d=6, seed=17):
+    """A reference iResBlock on a 6-64-64-6 Sin fc net (train_tabular-style), one training backward."""
+    torch.manual_seed(77)
+    lin = lambda a, b: mg.base_layers.get_linear(a, b, coeff=0.97, n_iterations=None, atol=1e-3, rtol=1e-3,
+                                                 domain=2, codomain=2)
+    nnet = torch.nn.Sequential(lin(d, 64), mg.base_layers.Sin(), lin(64, 64), mg.base_layers.Sin(), lin(64, d))
+    blk = mg.layers.iResBlock(nnet, n_dist='geometric', n_exact_terms=2, neumann_grad=neumann,
+                              grad_in_forward=mem_eff, brute_force=False)
+    blk.train()
+    x = syn.tabular_batch(B, d, seed=31).float()
+    out = {'sd:' + k: v.detach().numpy().copy() for k, v in blk.state_dict().items()}
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    y, delta = blk(x, torch.zeros(B, 1))
+    logpx = (-0.5 * np.log(2 * np.pi) - y.pow(2) / 2).sum(1, keepdim=True) - delta
+    loss = -torch.mean(logpx)
+    loss.backward()
+    out.update(x=x.detach().numpy().astype(np.float32), seed=np.int64(seed), loss=np.float64(loss.item()),
+               logpx=logpx.detach().view(-1).numpy().astype(np.float64))
+    for pname, p in blk.named_parameters():
+        if p.grad is not None:
+            out['g:' + pname] = p.grad.detach().numpy().astype(np.float32).ravel()
+    path = os.path.join(HERE, name + '.npz')
+    np.savez_compressed(path, **out)
+    print('%-26s loss=%.8f -> %s (%d KB)' % (name, loss.item(), os.path.basename(path), os.path.getsize(path) // 1024))
+
+
 CASES = {
+    'ires_neumann_train_b64': lambda: run_ires_case('ires_neumann_train_b64', True, True),
+    'ires_basic_train_b64': lambda: run_ires_case('ires_basic_train_b64', False, False),
     'cifar_small_train_b2': lambda: run_train_case('cifar_small_train_b2', syn.CIFAR10_SMALL,
                                                    syn.image_batch(2, seed=21), seed=5),
     'power_train_grad_b64': lambda: run_train_case('power_train_grad_b64', syn.POWER, syn.tabular_batch(64, 6, seed=8),

@@ -93,3 +93,33 @@ def test_training_gradients_match_reference(golden_dir, name, arch):
     assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
     n = _check_grads(m, g)
     assert n == len([k for k in g.files if k.startswith('g:') or k.startswith('gs:')])
+
+
+@pytest.mark.parametrize('name,neumann,mem_eff', [('ires_neumann_train_b64', True, True),
+                                                  ('ires_basic_train_b64', False, False)])
+def test_iresblock_training_gradients_match_reference(golden_dir, name, neumann, mem_eff):
+    """iResBlock (iresblock.py:13-258) training backward: Neumann + memory-efficient estimator and the
+    basic series with the graph, on a 6-64-64-6 Sin fc net; same state dict as the reference run."""
+    from lib.layers import iResBlock
+    from lib.layers.base import Sin, get_linear
+    path = os.path.join(golden_dir, name + '.npz')
+    if not os.path.exists(path):
+        pytest.skip('missing fixture ' + name)
+    g = np.load(path)
+    lin = lambda a, b: get_linear(a, b, coeff=0.97, n_iterations=None, atol=1e-3, rtol=1e-3, domain=2, codomain=2)
+    nnet = torch.nn.Sequential(lin(6, 64), Sin(), lin(64, 64), Sin(), lin(64, 6))
+    blk = iResBlock(nnet, n_dist='geometric', n_exact_terms=2, neumann_grad=neumann, grad_in_forward=mem_eff,
+                    brute_force=False)
+    sd = {k[3:]: torch.from_numpy(np.asarray(g[k])) for k in g.files if k.startswith('sd:')}
+    blk.load_state_dict(sd, strict=True)
+    blk = blk.to(DEV).train()
+    x = torch.from_numpy(g['x']).to(DEV)
+    set_probe_mode('reference')
+    np.random.seed(int(g['seed']))
+    torch.manual_seed(int(g['seed']))
+    y, delta = blk(x, torch.zeros(x.shape[0], 1, device=DEV))
+    logpx = (-0.5 * np.log(2 * np.pi) - y.pow(2) / 2).sum(1, keepdim=True) - delta
+    loss = -torch.mean(logpx)
+    loss.backward()
+    assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
+    assert _check_grads(blk, g) == len([k for k in g.files if k.startswith('g:')])
