@@ -36,6 +36,11 @@ from lib.configs import build_flow, imblocks  # noqa: E402
 from lib.density import image_logpx  # noqa: E402
 from lib.layers import set_probe_mode  # noqa: E402
 
+METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs are labelled alike
+    'cifar10': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 density eval at 1/8 GPU',
+    'cifar10_small': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 (idim 64) density eval',
+    'celebahq256': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CelebA-HQ 256 density eval',
+}
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
 HBM_PEAK_GBS = 8000.0
 
@@ -142,7 +147,7 @@ def main():
             traffic = None
 
     out = {
-        'metric': 'samples/sec (whole node) + bits/dim delta vs ref, CIFAR10 density eval',
+        'metric': METRIC[args.config],
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',

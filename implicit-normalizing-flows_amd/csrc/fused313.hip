@@ -27,11 +27,14 @@
 
 namespace inf {
 
-// LDS per workgroup: 64-pixel tiles take the whole 160 KiB (one workgroup per CU); 32-pixel tiles
-// take 80 KiB so two workgroups share a CU and overlap each other's staging / epilogues / barriers.
-template <int F_BN>
-constexpr int lds_floats() { return F_BN == 64 ? 40960 : 20480; }
-constexpr int lds_floats_rt(int bn) { return bn == 64 ? 40960 : 20480; }
+// Three variants (LDS per workgroup):
+//   net313_kernel    64-pixel tiles, the whole 160 KiB (one workgroup per CU)
+//   net313_kernel_h  32-pixel tiles in 80 KiB and <= 128 VGPRs: two workgroups share a CU and overlap
+//                    each other's staging / epilogues / barriers (small grids)
+//   net313_kernel_w  32-pixel tiles with the whole 160 KiB: wide nets whose halo tile does not fit
+//                    next to a 64-pixel activation tile (9C up to ~1.7K tap rows: CelebA-HQ 64x64 and
+//                    32x32 scales)
+constexpr int LDS_FULL = 40960, LDS_HALF = 20480;
 
 __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   const f32x4 v0 = *reinterpret_cast<const f32x4*>(base);
@@ -45,9 +48,8 @@ __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;
 }
 
-template <int TM, int MODE, int F_BN>
+template <int TM, int MODE, int F_BN, int F_LDS_FLOATS>
 __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
-  constexpr int F_LDS_FLOATS = lds_floats<F_BN>();
   constexpr int HID = 8 * 32 * TM;
   constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
   // two independent nets (the x- and z-branch of an imBlock) can share one launch
@@ -365,10 +367,16 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     const int kts = nkt / ksplit;
     const int njobs = ntask * ksplit;
     float* part = smem;          // reuse t after the barrier below (ksplit > 1 only)
+    float* Y = a.Y + (long)img * a.M3 * P;
+    // rounds of 32 jobs (4 per wave); wide nets (9C > 32*32 tap rows per round) take several rounds.
+    // The split-K path only occurs with <= 8 jobs, i.e. in a single round.
+    const int nrounds = (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 31) / 32;   // _h: <= 32 jobs (variant_fits)
+    for (int round = 0; round < nrounds; ++round) {
+    const int jbase = round * 32;
     f32x16 cacc[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int job = wid + 8 * jj;
+      const int job = jbase + wid + 8 * jj;
 #pragma unroll
       for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
       if (job >= njobs) continue;
@@ -393,11 +401,10 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         tileC(kt + 1, c1);
       }
     }
-    float* Y = a.Y + (long)img * a.M3 * P;
     if (ksplit == 1) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int job = wid + 8 * jj;
+        const int job = jbase + wid + 8 * jj;
         if (job >= njobs) continue;
         const int rb = job / NB, b = job % NB;
         const int gcol = gp_rt(b);
@@ -430,35 +437,44 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         }
       }
     }
+    }   // rounds
   }
 }
 
 template <int TM, int MODE>
 __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
-  net313_body<TM, MODE, 64>(pr);
+  net313_body<TM, MODE, 64, LDS_FULL>(pr);
 }
 // two workgroups (16 waves) per CU: at most 128 VGPRs
 template <int TM, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void net313_kernel_h(Net313Pair pr) {
-  net313_body<TM, MODE, 32>(pr);
+  net313_body<TM, MODE, 32, LDS_HALF>(pr);
+}
+template <int TM, int MODE>
+__global__ __launch_bounds__(512) void net313_kernel_w(Net313Pair pr) {
+  net313_body<TM, MODE, 32, LDS_FULL>(pr);
 }
 
-static int tile_bn(int hid, int C, int H, int W, int bn) {
+enum { V64 = 0, VHALF = 1, VWIDE = 2 };
+
+static int tile_fits(int hid, int C, int H, int W, int bn, int ldsf) {
   const int P = H * W;
   const int seg = W < bn ? W : bn;
   if (P % bn != 0 || bn % seg != 0 || (W > bn && W % bn != 0)) return 0;
   const int rows = bn / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
   const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
-  if (need > lds_floats_rt(bn) - 16) return 0;            // last 16 floats: trace-partial slots
-  const long m3pad = (9L * C + 31) / 32 * 32;
-  if ((m3pad / 32) * (bn / 32) > 32) return 0;    // at most 4 phase-C jobs per wave
-  return 1;
+  return need <= ldsf - 16;                                // last 16 floats: trace-partial slots
+}
+static int variant_fits(int hid, int C, int H, int W, int v) {
+  if (v == V64) return tile_fits(hid, C, H, W, 64, LDS_FULL);
+  if (v == VHALF) return tile_fits(hid, C, H, W, 32, LDS_HALF) && (9L * C + 31) / 32 <= 32;   // one phase-C round
+  return tile_fits(hid, C, H, W, 32, LDS_FULL);
 }
 
 int net313_supported(int hid, int C, int H, int W) {
   if (hid != 512 && hid != 256) return 0;
-  return tile_bn(hid, C, H, W, 64) || tile_bn(hid, C, H, W, 32);
+  return variant_fits(hid, C, H, W, V64) || variant_fits(hid, C, H, W, VHALF) || variant_fits(hid, C, H, W, VWIDE);
 }
 
 // Launch one or two nets (same shape) as one grid.  The 64-pixel tile is used unless the grid would
@@ -471,10 +487,14 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     const char* e = getenv("INFLOW_FUSED_BN");            // tuning knob: 32 / 64 (default: auto)
     return e ? atoi(e) : 0;
   }();
-  int bn = 64;
-  if (!tile_bn(hid, a0.C, a0.H, a0.W, 64) || (nnets * a0.B * (P / 64) < 256 && tile_bn(hid, a0.C, a0.H, a0.W, 32)))
-    bn = 32;
-  if (force_bn && tile_bn(hid, a0.C, a0.H, a0.W, force_bn)) bn = force_bn;
+  // 64-pixel tiles unless the grid would leave CUs idle; then 32-pixel tiles two per CU; the wide
+  // variant when neither fits
+  const bool f64 = variant_fits(hid, a0.C, a0.H, a0.W, V64), fh = variant_fits(hid, a0.C, a0.H, a0.W, VHALF);
+  int var = f64 ? V64 : (fh ? VHALF : VWIDE);
+  if (var == V64 && nnets * a0.B * (P / 64) < 256 && fh) var = VHALF;
+  if (force_bn == 64 && f64) var = V64;
+  if (force_bn == 32 && fh) var = VHALF;
+  const int bn = var == V64 ? 64 : 32;
   Net313Pair pr;
   pr.a[0] = args[0];
   pr.a[1] = args[nnets - 1];
@@ -489,10 +509,11 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const unsigned nb = (unsigned)(pr.nb0 * nnets);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define L313(TM_, MODE_, BN_)                                                                   \
-  do {                                                                                          \
-    if (BN_ == 64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr); \
-    else hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);         \
+#define L313(TM_, MODE_, BN_)                                                                     \
+  do {                                                                                            \
+    if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);   \
+    else if (var == VHALF) hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr); \
+    else hipLaunchKernelGGL((net313_kernel_w<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);           \
   } while (0)
 #define L313M(TM_, BN_)                                \
   do {                                                 \
@@ -500,11 +521,8 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     else if (mode == MODE_SAVE) L313(TM_, MODE_SAVE, BN_); \
     else L313(TM_, MODE_VJP, BN_);                     \
   } while (0)
-  if (hid == 512) {
-    if (bn == 64) L313M(2, 64); else L313M(2, 32);
-  } else {
-    if (bn == 64) L313M(1, 64); else L313M(1, 32);
-  }
+  if (hid == 512) L313M(2, bn);
+  else L313M(1, bn);
 #undef L313M
 #undef L313
   INF_CHECK_LAUNCH();
@@ -513,7 +531,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     const double fA = 2.0 * hid * 9.0 * a0.C, fB = 2.0 * hid * hid;
     const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
     const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
-    prof_end_launch(s, 500 + (bn == 32 ? 10 : 0) + mode, npx * (fA + fB + fC), bytes);   // 51x: 2-per-CU variant
+    prof_end_launch(s, 500 + 10 * var + mode, npx * (fA + fB + fC), bytes);   // 50x / 51x (_h) / 52x (_w)
   }
   return INF_OK;
 }

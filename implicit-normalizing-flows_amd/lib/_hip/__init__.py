@@ -291,8 +291,8 @@ def profile_end():
 
 def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
-    if 500 <= tag < 520:     # 50x: 64-pixel tiles (net313_kernel), 51x: 32-pixel, 2 per CU (net313_kernel_h)
-        return 'net313_kernel%s<%s>' % ('_h' if tag >= 510 else '', ['EVAL', 'SAVE', 'VJP'][tag % 10])
+    if 500 <= tag < 530:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide)
+        return 'net313_kernel%s<%s>' % (['', '_h', '_w'][(tag - 500) // 10], ['EVAL', 'SAVE', 'VJP'][tag % 10])
     if tag < 1000:
         modes = {0: 'PLAIN', 1: 'EMBED', 2: 'RESID', 3: 'RECOMP', 4: 'VJP'}
         return 'conv_out_kernel<%d> mode %s' % (tag % 10, modes.get((tag - 900) // 10, '?'))

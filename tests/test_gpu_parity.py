@@ -315,3 +315,54 @@ def test_power_iteration_matches_host(kind):
     assert abs(dev.scale.item() - host.scale.item()) <= 1e-5 * abs(host.scale.item())
     w_host = host.compute_weight(update=False)
     np.testing.assert_allclose(w_dev.cpu().numpy(), w_host.detach().numpy(), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize('C,H', [(48, 64), (192, 32)])
+def test_fused_wide_variant_matches_generic(C, H, monkeypatch):
+    """CelebA-HQ 256 scales (9C tap rows up to 1728, 64x64 / 32x32): the 32-pixel full-LDS variant
+    (net313_kernel_w, several phase-C rounds) against the generic GEMM chain, workspace and LDS
+    poisoned with NaN before every call."""
+    from lib.layers.base import InducedNormConv2d, Swish
+    torch.manual_seed(2)
+    B = 2
+    conv = lambda a, b, k: InducedNormConv2d(a, b, k, 1, k // 2, coeff=0.9, atol=1e-3, rtol=1e-3)
+    seq = torch.nn.Sequential(Swish(), conv(C, 512, 3), Swish(), conv(512, 512, 1), Swish(), conv(512, C, 3)).to(DEV)
+    with torch.no_grad():
+        seq(torch.zeros(1, C, H, H, device=DEV))             # lazy u/v (engine power iteration)
+        for m in seq:
+            if isinstance(m, Swish):
+                m.beta.fill_(0.3)
+    x = (torch.randn(B, C, H, H) * 0.5).to(DEV)
+    v = torch.randn(B, C, H, H).to(DEV)
+    outs = {}
+    for mode in ('fused', 'generic'):
+        monkeypatch.setenv('INFLOW_NO_FUSED', '1' if mode == 'generic' else '0')
+        net = _hip.NativeNet(_hip.net_entries(seq), (C, H, H), x.device)   # fresh: reads INFLOW_NO_FUSED
+        assert net.handle
+        stream = _hip.stream_of(x)
+        net.refresh_if_needed(stream)
+        ws = torch.empty(net.ws_bytes(B), dtype=torch.uint8, device=DEV)
+
+        def poison():
+            ws.fill_(255)
+            _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
+        y, g = torch.empty_like(x), torch.empty_like(x)
+        poison()
+        _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
+                                           stream), 'fwd')
+        poison()
+        _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(x), _hip.ptr(v), _hip.ptr(g), B, _hip.ptr(ws),
+                                       ws.numel(), stream), 'vjp')
+        co = np.array([(-1) ** (k + 1) / k for k in range(1, 7)], dtype=np.float32)
+        ld = torch.empty(B, device=DEV)
+        poison()
+        _hip.check(net.lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(torch.sign(v)),
+                                             co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 6, _hip.ptr(ld), B,
+                                             _hip.ptr(ws), ws.numel(), stream), 'series')
+        torch.cuda.synchronize()
+        outs[mode] = (y, g, ld)
+        del net
+    for a in outs['fused']:
+        assert torch.isfinite(a).all()
+    for a, b in zip(outs['fused'], outs['generic']):
+        _close(a, b, rel=1e-5)
