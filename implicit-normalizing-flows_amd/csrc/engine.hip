@@ -116,6 +116,7 @@ struct Bufs {
   float *h0, *h1, *Y;
   std::vector<float*> D;   // saved activation derivatives, one per hidden layer
   float *xin, *xemb, *fx, *xa, *xb, *ga, *gb, *upd, *dx, *dg, *lowest, *va, *vb, *eps_t, *zero, *tmp;
+  float *fcur, *flow;      // root solve: f(z) of the latest residual evaluation / of the lowest iterate
   float *U, *VT;
   float *ext0, *ext1;
   double *part, *bpart, *sumsq;
@@ -145,7 +146,7 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   b.D.resize(n->L.size() > 0 ? n->L.size() - 1 : 0);
   for (auto& p : b.D) p = w.take<float>(Hs);
   float** vecs[] = {&b.xin, &b.xemb, &b.fx, &b.xa, &b.xb, &b.ga, &b.gb, &b.upd,
-                    &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp};
+                    &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp, &b.fcur, &b.flow};
   for (float** v : vecs) *v = w.take<float>(E);
   b.U = w.take<float>((size_t)T * E);
   b.VT = w.take<float>((size_t)T * E);
@@ -365,6 +366,7 @@ int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, 
   a.in2 = gprev;
   a.out0 = gout;
   a.out1 = dg;
+  a.out2 = bf.fcur;
   a.partial = bf.part;
   a.nchunk = bf.nchunk;
   INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
@@ -412,7 +414,7 @@ using ResidFn = std::function<int(const float* x, float* gout, float* dg, const 
 
 // broyden.py:123-193 with the residual as a callback; the result (lowest iterate) is in bf.lowest.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
-                 std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s) {
+                 std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
@@ -433,6 +435,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
   INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  if (keep_f) INF_HIP(hipMemcpyAsync(bf.flow, bf.fcur, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
   // update = -gx; x_est = x0 + update
   INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
   INF_TRY(launch_axpy_step(x, bf.upd, xn, bf.dx, (long)E, s));
@@ -445,6 +448,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     trace.push_back(obj);
     if (obj < lowest) {                                               // :159-162
       INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+      if (keep_f) INF_HIP(hipMemcpyAsync(bf.flow, bf.fcur, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
       lowest = obj;
       lowest_step = nstep;
       lowest_ss = ss;
@@ -501,7 +505,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
     return eval_resid(f, x, x, bf.xemb, gout, dg, gprev, B, bf, ss, s);
   };
-  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s));
+  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -807,8 +811,17 @@ int inf_imblock_forward(InfNet* nx, InfNet* nz, const float* x, float* z, int B,
   Bufs bf;
   if (!ws || carve(nx, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
   const float* xi;
-  INF_TRY(root_find_common(nz, nx, x, B, T, eps, stats, nullptr, bf, &xi, s));
-  // z = (nnet_x(x) - nnet_z(z*)) + x   (implicit_block.py:227)
+  InfBroydenStats st;
+  INF_TRY(root_find_common(nz, nx, x, B, T, eps, &st, nullptr, bf, &xi, s));
+  if (stats) *stats = st;
+  // z = (nnet_x(x) - nnet_z(z*)) + x   (implicit_block.py:227).  nnet_z(z*) was evaluated by the residual
+  // that produced the lowest iterate (same input, same kernel: the same bits) and kept in bf.flow; only
+  // after the Banach fallback (prot_break) is it evaluated again.
+  if (!st.prot_break) {
+    INF_TRY(glue_recomp(bf.fx, bf.flow, xi, nx->fc ? bf.tmp : z, (long)B * nx->d, s));
+    if (nx->fc) INF_TRY(to_boundary(nx, bf.tmp, z, B, s));
+    return INF_OK;
+  }
   OutArgs a;
   memset(&a, 0, sizeof(a));
   a.in0 = bf.fx;

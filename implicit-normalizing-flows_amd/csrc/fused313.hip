@@ -175,12 +175,30 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   const long plane = (long)img * HID * P;           // sample offset of HID-channel tensors
   const int rbw = wid * TM;                          // this wave's first 32-row block
   auto row_of = [&](int m, int r) { return (rbw + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh; };
-  // HID-channel HBM tensors: one base pointer per (row block, column); element r of the MFMA tile
-  // is at base[roff(r)] with the wave-uniform row offset roff(r) = ((r&3) + 8(r>>2)) * P.
-  auto hid_base = [&](float* base, int m, int b) {
-    return base + plane + (long)((rbw + m) * 32 + 4 * lh) * P + gp[b];
+  // The activation derivatives d1, d2 of a fused net (written by SAVE, read by VJP -- always with the
+  // same tile variant) are stored in MFMA-fragment order: for tile `bid`, row block (rbw + m) and
+  // 32-pixel column b, lane l's 16 accumulator values are 64 contiguous bytes.  One (m, b) is then
+  // 4 x dwordx4 per lane (a wave reads 4 KiB contiguous) instead of 16 row-strided dword loads.
+  auto dfrag = [&](float* base, int m, int b) {
+    return base + (((long)bid * (8 * TM) + rbw + m) * NB + b) * 1024 + lane * 16;
   };
-  auto roff = [&](int r) { return ((r & 3) + 8 * (r >> 2)) * P; };
+  auto load_d = [&](const float* base, int m, int b, float (&o)[16]) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(dfrag(const_cast<float*>(base), m, b));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = q[j];
+      o[4 * j] = v.x;
+      o[4 * j + 1] = v.y;
+      o[4 * j + 2] = v.z;
+      o[4 * j + 3] = v.w;
+    }
+  };
+  auto store_d = [&](float* base, int m, int b, const float (&o)[16]) {
+    f32x4* q = reinterpret_cast<f32x4*>(dfrag(base, m, b));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = f32x4{o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]};
+  };
+  (void)plane;
 
   // VJP: prefetch the phase-A multiplier d2 (retired by the phase-A loop's waits)
   float dmul[TM][NB][16];
@@ -188,11 +206,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-          const float* src = hid_base(a.d2, m, b);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) dmul[m][b][r] = src[roff(r)];
-      }
+      for (int b = 0; b < NB; ++b) load_d(a.d2, m, b, dmul[m][b]);
   }
   __syncthreads();
   if (a.dot_part && tid == 0) {
@@ -260,7 +274,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        float* dst = (MODE == MODE_SAVE) ? hid_base(a.d1, m, b) : nullptr;
+        float dv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int o = row_of(m, r);
@@ -270,10 +284,11 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           } else {
             const float z = acc[m][b][r] + a.b1[o];
             v = swish_f(z, sp1);
-            if constexpr (MODE == MODE_SAVE) dst[roff(r)] = swish_d(z, sp1);
+            if constexpr (MODE == MODE_SAVE) dv[r] = swish_d(z, sp1);
           }
           t[o * F_BN + b * 32 + li] = v;
         }
+        if constexpr (MODE == MODE_SAVE) store_d(a.d1, m, b, dv);
       }
   }
   __syncthreads();
@@ -317,24 +332,20 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        float* dst = hid_base(a.d2, m, b);
+        float dv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dst[roff(r)] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
+        for (int r = 0; r < 16; ++r) dv[r] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
+        store_d(a.d2, m, b, dv);
       }
     return;
   } else {
-    // epilogue B -> t (after every wave finished reading t).  VJP: the multiplier d1 is loaded here,
-    // not prefetched across the phase-B loop (64 more live registers there would spill).
+    // epilogue B -> t (after every wave finished reading t); VJP loads its multiplier d1 here (issuing it
+    // inside the phase-B loop measured slower: the loads contend with every CU's operand streams)
     if constexpr (MODE == MODE_VJP) {
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
-        {
-          const float* src = hid_base(a.d1, m, b);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) dmul[m][b][r] = src[roff(r)];
-        }
+        for (int b = 0; b < NB; ++b) load_d(a.d1, m, b, dmul[m][b]);
     }
     const float sp2 = (MODE == MODE_EVAL) ? softplus_f(*a.beta2) : 0.f;
 #pragma unroll

@@ -175,6 +175,17 @@ int glue_add(const float* a, const float* b, float* out, long n, hipStream_t s) 
   return INF_OK;
 }
 
+__global__ void recomp_kernel(const float* fx, const float* fz, const float* x, float* out, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (fx[i] - fz[i]) + x[i];
+}
+// z = (nnet_x(x) - nnet_z(z*)) + x from the stored net outputs (implicit_block.py:227)
+int glue_recomp(const float* fx, const float* fz, const float* x, float* out, long n, hipStream_t s) {
+  hipLaunchKernelGGL(recomp_kernel, GRID1(n), 0, s, fx, fz, x, out, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // 160 KiB of LDS per workgroup, one workgroup per CU at a time; 8 waves of 4 per CU cover every CU.
 __global__ __launch_bounds__(1024) void poison_lds_kernel(float* sink) {
   __shared__ float lds[40960];

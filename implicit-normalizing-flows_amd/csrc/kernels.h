@@ -51,6 +51,7 @@ struct OutArgs {
   const float* in2;
   float* out0;
   float* out1;
+  float* out2;            // OM_RESID (optional): the net output f(z) itself
   const float* pre_beta;  // OM_VJP: multiply by swish'(in1) (preact input derivative)
   double* partial;        // (B, nchunk) per-sample partial sums (OM_RESID: g^2, OM_VJP: v.eps)
   int nchunk;
@@ -130,8 +131,8 @@ struct Net313Args {
   const float* beta1;
   const float* b2;
   const float* beta2;
-  float* d1;              // (B, HID, H, W) swish'(a1): SAVE writes, VJP reads
-  float* d2;              // (B, HID, H, W) swish'(a2)
+  float* d1;              // swish'(a1), B*HID*H*W floats in MFMA-fragment order (fused313.hip dfrag)
+  float* d2;              // swish'(a2), same layout
   float* Y;               // (B, M3, H, W) packed taps
   int B, C, H, W, seg;
   // VJP series chaining (conv_out folded into the next term's halo staging):

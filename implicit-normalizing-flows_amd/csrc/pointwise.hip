@@ -22,7 +22,7 @@ int out_nchunk(int per_sample) { return (per_sample + OUT_CH - 1) / OUT_CH; }
 // then (implicit_block.py:60,72,227,422-423):
 //   OM_PLAIN : out0 = s + bias
 //   OM_EMBED : out0 = a = s + bias (= nnet_x(x));  out1 = a + x   (x_embed)
-//   OM_RESID : out0 = g = (x_embed - a) - z;  out1 = g - g_prev;  partial += g^2
+//   OM_RESID : out0 = g = (x_embed - a) - z;  out1 = g - g_prev;  [out2 = a];  partial += g^2
 //   OM_RECOMP: out0 = (fx - a) + x
 //   OM_VJP   : out0 = v = s (* swish'(x_in) for preact nets);  partial += v * eps
 // ------------------------------------------------------------------------------------------
@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void conv_out_kernel(OutArgs a) {
         const float gx = (a.in0[ei] - v) - a.in1[ei];
         a.out0[ei] = gx;
         if (a.in2) a.out1[ei] = gx - a.in2[ei];
+        if (a.out2) a.out2[ei] = v;
         acc += (double)gx * (double)gx;
         break;
       }
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(256) void fc_out_kernel(OutArgs a, int batch) {
         const float gx = (a.in0[ei] - v) - a.in1[ei];
         a.out0[ei] = gx;
         if (a.in2) a.out1[ei] = gx - a.in2[ei];
+        if (a.out2) a.out2[ei] = v;
         acc += (double)gx * (double)gx;
         break;
       }
