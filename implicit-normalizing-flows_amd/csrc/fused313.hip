@@ -48,9 +48,10 @@ __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;
 }
 
-template <int TM, int MODE, int F_BN, int F_LDS_FLOATS>
+template <int TM, int MODE, int F_BN, int F_LDS_FLOATS, int NW = 8>
 __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
-  constexpr int HID = 8 * 32 * TM;
+  constexpr int NT = 64 * NW;                        // threads per workgroup
+  constexpr int HID = NW * 32 * TM;
   constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
   // two independent nets (the x- and z-branch of an imBlock) can share one launch
   const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
@@ -90,13 +91,13 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     // 4 halo elements per pass with unconditional (clamped-address) loads: 36 tap loads in flight
     // per thread instead of one bounds-checked chain per element.
     constexpr int SU = 4;
-    for (int i0 = tid; i0 < vhz; i0 += 512 * SU) {
+    for (int i0 = tid; i0 < vhz; i0 += NT * SU) {
       float tv[SU][9], xm[SU], ev[SU];
       int ok[SU];
       long ee[SU];
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
-        const int i = i0 + u * 512;
+        const int i = i0 + u * NT;
         const int ic = i < vhn ? i : 0;
         const int c = ic / (RH * CW), rr = ic - c * RH * CW;
         const int hy = rr / CW, hx = rr - hy * CW;
@@ -118,7 +119,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       }
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
-        const int i = i0 + u * 512;
+        const int i = i0 + u * NT;
         float v = 0.f;
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) v += tv[u][tp];
@@ -129,7 +130,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       }
     }
   } else {
-    for (int i = tid; i < vhz; i += 512) {
+    for (int i = tid; i < vhz; i += NT) {
       float v = 0.f;
       if (i < vhn) {
         const int c = i / (RH * CW), rr = i - c * RH * CW;
@@ -149,7 +150,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     const double w = wave_sum(dacc);
     if (lane == 0) red[wid] = w;
   }
-  for (int k = tid; k < a.K1pad; k += 512) {
+  for (int k = tid; k < a.K1pad; k += NT) {
     int o = vhn;                                    // zero slot for the K padding
     if (k < 9 * a.C) {
       const int c = k / 9, tt = k - c * 9;
@@ -180,7 +181,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // 32-pixel column b, lane l's 16 accumulator values are 64 contiguous bytes.  One (m, b) is then
   // 4 x dwordx4 per lane (a wave reads 4 KiB contiguous) instead of 16 row-strided dword loads.
   auto dfrag = [&](float* base, int m, int b) {
-    return base + (((long)bid * (8 * TM) + rbw + m) * NB + b) * 1024 + lane * 16;
+    return base + (((long)bid * (NW * TM) + rbw + m) * NB + b) * 1024 + lane * 16;
   };
   auto load_d = [&](const float* base, int m, int b, float (&o)[16]) {
     const f32x4* q = reinterpret_cast<const f32x4*>(dfrag(const_cast<float*>(base), m, b));
@@ -212,7 +213,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   if (a.dot_part && tid == 0) {
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) s += red[w];
+    for (int w = 0; w < NW; ++w) s += red[w];
     a.dot_part[(long)img * a.dot_nchunk + tile] = s;
   }
 
@@ -373,7 +374,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     const int nrb = a.M3pad / 32;
     const int ntask = nrb * NB;
     int ksplit = 1;
-    while (ntask * ksplit * 2 <= 8 && ksplit < pr.max_ksplit) ksplit *= 2;
+    while (ntask * ksplit * 2 <= NW && ksplit < pr.max_ksplit) ksplit *= 2;
     constexpr int nkt = HID / 16;
     const int kts = nkt / ksplit;
     const int njobs = ntask * ksplit;
@@ -381,13 +382,13 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     float* Y = a.Y + (long)img * a.M3 * P;
     // rounds of 32 jobs (4 per wave); wide nets (9C > 32*32 tap rows per round) take several rounds.
     // The split-K path only occurs with <= 8 jobs, i.e. in a single round.
-    const int nrounds = (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 31) / 32;   // _h: <= 32 jobs (variant_fits)
+    const int nrounds = (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 4 * NW - 1) / (4 * NW);   // half-LDS: 1 (variant_fits)
     for (int round = 0; round < nrounds; ++round) {
-    const int jbase = round * 32;
+    const int jbase = round * 4 * NW;
     f32x16 cacc[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int job = jbase + wid + 8 * jj;
+      const int job = jbase + wid + NW * jj;
 #pragma unroll
       for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
       if (job >= njobs) continue;
@@ -415,7 +416,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     if (ksplit == 1) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int job = jbase + wid + 8 * jj;
+        const int job = jbase + wid + NW * jj;
         if (job >= njobs) continue;
         const int rb = job / NB, b = job % NB;
         const int gcol = gp_rt(b);
@@ -429,14 +430,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       __syncthreads();
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int job = wid + 8 * jj;
+        const int job = wid + NW * jj;
         if (job >= njobs) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) part[(job * 16 + r) * 64 + lane] = cacc[jj][r];
       }
       __syncthreads();
       // one wave per task sums its ksplit partials
-      for (int task = wid; task < ntask; task += 8) {
+      for (int task = wid; task < ntask; task += NW) {
         const int rb = task / NB, b = task % NB;
         const int gcol = gp_rt(b);
 #pragma unroll
@@ -465,7 +466,6 @@ template <int TM, int MODE>
 __global__ __launch_bounds__(512) void net313_kernel_w(Net313Pair pr) {
   net313_body<TM, MODE, 32, LDS_FULL>(pr);
 }
-
 enum { V64 = 0, VHALF = 1, VWIDE = 2 };
 
 static int tile_fits(int hid, int C, int H, int W, int bn, int ldsf) {
@@ -505,6 +505,11 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   if (var == V64 && nnets * a0.B * (P / 64) < 256 && fh) var = VHALF;
   if (force_bn == 64 && f64) var = V64;
   if (force_bn == 32 && fh) var = VHALF;
+  static const int force_var = [] {
+    const char* e = getenv("INFLOW_FUSED_VARIANT");       // tuning knob: 0 64-px, 1 _h, 2 _w
+    return e ? atoi(e) : -1;
+  }();
+  if (force_var >= 0 && variant_fits(hid, a0.C, a0.H, a0.W, force_var)) var = force_var;
   const int bn = var == V64 ? 64 : 32;
   Net313Pair pr;
   pr.a[0] = args[0];
