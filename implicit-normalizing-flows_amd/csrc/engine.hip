@@ -91,6 +91,10 @@ struct InfNet {
   bool fused = false;
   int fhid = 0, K1pad = 0, M3 = 0, M3pad = 0;
   float *F1f = nullptr, *F1b = nullptr, *F2f = nullptr, *F2b = nullptr, *F3f = nullptr, *F3b = nullptr;
+  // f(0) of a conv net (the same image for every sample: zero input, zero padding), cached for the first
+  // Broyden residual; computed by a launch of the same batch size (same tile variant -> same bits)
+  float* f0 = nullptr;
+  int f0_batch = -1;
 };
 
 namespace {
@@ -497,12 +501,34 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   return INF_OK;
 }
 
+// f(0) for sample 0 of a conv net, computed once per (weights, batch size) with a B-sized launch
+static int ensure_f0(InfNet* f, int B, Bufs& bf, hipStream_t s) {
+  if (f->fc || f->f0_batch == B) return INF_OK;
+  const size_t per = (size_t)f->d;
+  if (!f->f0 && hipMalloc(&f->f0, per * sizeof(float)) != hipSuccess) return INF_ERR_HIP;
+  INF_HIP(hipMemsetAsync(bf.zero, 0, sizeof(float) * per * B, s));
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.out0 = bf.fcur;
+  INF_TRY(run_forward(f, bf.zero, B, bf, OM_PLAIN, &a, s));
+  INF_HIP(hipMemcpyAsync(f->f0, bf.fcur, per * sizeof(float), hipMemcpyDeviceToDevice, s));
+  f->f0_batch = B;
+  return INF_OK;
+}
+
 int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
                   Bufs& bf, hipStream_t s) {
   const size_t E = (size_t)B * f->d;
   InfBroydenStats stats;
   std::vector<double> lowest_ss;
+  INF_TRY(ensure_f0(f, B, bf, s));
+  bool first = !f->fc;           // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached
   const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
+    if (first) {
+      first = false;
+      INF_TRY(launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s));
+      return read_sumsq(f, B, bf, ss, s);
+    }
     return eval_resid(f, x, x, bf.xemb, gout, dg, gprev, B, bf, ss, s);
   };
   INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
@@ -710,6 +736,7 @@ int inf_net_destroy(InfNet* n) {
   if (!n) return INF_OK;
   if (n->dev) (void)hipFree(n->dev);
   if (n->scratch) (void)hipFree(n->scratch);
+  if (n->f0) (void)hipFree(n->f0);
   delete n;
   return INF_OK;
 }
@@ -717,6 +744,7 @@ int inf_net_destroy(InfNet* n) {
 int inf_net_refresh(InfNet* n, void* stream) {
   if (!n) return INF_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  n->f0_batch = -1;
   for (auto& w : n->L) {
     const int H = n->fc ? 1 : (w.ks == 1 ? 1 : n->H), Wd = n->fc ? 1 : (w.ks == 1 ? 1 : n->W);
     INF_TRY(launch_sigma(w.W, w.u, w.v, w.cout, w.cin, w.ks, H, Wd, w.coeff, w.factor,

@@ -101,6 +101,33 @@ int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
   return INF_OK;
 }
 
+// First Broyden residual from the cached f(0) (conv nets): v = f0[i] for every sample,
+// g = (x_embed - v) - z exactly as conv_out's OM_RESID, fcur = v, per-sample partial sums of g^2.
+__global__ __launch_bounds__(256) void resid_bcast_kernel(const float* f0, const float* xemb, const float* z, float* g,
+                                                          float* fcur, double* partial, int per, int nchunk) {
+  __shared__ double red[16];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const long base = (long)b * per;
+  const int lo = chunk * OUT_CH, hi = min(per, lo + OUT_CH);
+  double acc = 0.0;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const float v = f0[i];
+    const float gx = (xemb[base + i] - v) - z[base + i];
+    g[base + i] = gx;
+    fcur[base + i] = v;
+    acc += (double)gx * (double)gx;
+  }
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[(long)b * nchunk + chunk] = t;
+}
+int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
+                       int batch, int per, int nchunk, hipStream_t s) {
+  hipLaunchKernelGGL(resid_bcast_kernel, dim3(out_nchunk(per), batch), dim3(256), 0, s, f0, xemb, z, g, fcur,
+                     partial, per, nchunk);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // Implicit-backward residual (implicit_block.py:186-190): g = (y + v) - grad with v = y^T J (the VJP),
 // dg = g - gprev (gprev may be null), per-sample partial sums of g^2.
 // Conv layout (B, d): grid (nchunk, B), partial[b * nchunk + chunk].  fc layout (d, B): one thread per
