@@ -908,13 +908,20 @@ int inf_imblock_backward(InfNet* nx, InfNet* nz, const float* z, const float* x,
 // the last term's taps go through conv_out.  Series slabs: part[k][b][snchunk] (zeroed first: the
 // fused kernel fills one entry per tile, conv_out one per 1024-element chunk).
 int series_fused(InfNet* const* nets, const float* const* xs, const float* const* es, int nn, const float* coeff,
-                 int n_terms, float* const* outs, int B, Bufs* bfs, hipStream_t s) {
+                 int n_terms, float* const* outs, int B, Bufs* bfs, hipStream_t s, unsigned save_mask = 3u) {
   Net313Args args[2];
   for (int i = 0; i < nn; ++i) {
     args[i] = net313_args(nets[i], xs[i], B, bfs[i], false);
     INF_HIP(hipMemsetAsync(bfs[i].part, 0, sizeof(double) * n_terms * B * bfs[i].snchunk, s));
   }
-  INF_TRY(launch_net313_multi(args, nn, nets[0]->fhid, MODE_SAVE, s));
+  // activation derivatives (in the pair's tile layout); a net whose d1/d2 are already saved is skipped
+  const unsigned all = (1u << nn) - 1u;
+  if ((save_mask & all) == all) {
+    INF_TRY(launch_net313_multi(args, nn, nets[0]->fhid, MODE_SAVE, s));
+  } else {
+    for (int i = 0; i < nn; ++i)
+      if (save_mask & (1u << i)) INF_TRY(launch_net313_multi(&args[i], 1, nets[0]->fhid, MODE_SAVE, s, nn));
+  }
   for (int k = 0; k < n_terms; ++k) {
     for (int i = 0; i < nn; ++i) {
       InfNet* n = nets[i];
@@ -957,6 +964,63 @@ int series_fused(InfNet* const* nets, const float* const* xs, const float* const
   for (int i = 0; i < nn; ++i)
     INF_TRY(launch_series_combine(bfs[i].part, coeff, n_terms, B, bfs[i].snchunk, outs[i], s));
   return INF_OK;
+}
+
+// Whole eval pass of an imBlock on fused nets (implicit_block.py:220-234 + 245-322 in eval): the x-net's
+// x_embed launch also saves its activation derivatives at x (MODE_EVALSAVE), Broyden solves for z*,
+// z = (f_x(x) - f_z(z*)) + x, then the paired power series of both branches with only the z-net's SAVE.
+int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const float* eps_x, const float* eps_z,
+                     const float* coeff, int n_terms, float* logdet_x, float* logdet_z, int B, int T, double eps,
+                     InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
+  if (!nx || !nz || !x || !z || !eps_x || !eps_z || !coeff || !logdet_x || !logdet_z || B <= 0 || T <= 0 || T > 64 ||
+      n_terms < 1 || n_terms > SERIES_MAX || !same_shape(nx, nz))
+    return INF_ERR_INVALID;
+  if (!(nx->fused && nz->fused && nx->fhid == nz->fhid)) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t half = ws_need(nx, B, T);
+  if (!ws || ws_bytes < half + ws_need(nz, B, 1)) return INF_ERR_WORKSPACE;
+  char* w0 = reinterpret_cast<char*>(ws);
+  Bufs bfa, bfb;
+  carve(nx, B, T, w0, half, bfa);
+  carve(nz, B, 1, w0 + half, ws_bytes - half, bfb);
+  // x_embed = f_x(x) + x, saving f_x's derivatives at x in the pair layout (implicit_block.py:71)
+  {
+    Net313Args f = net313_args(nx, x, B, bfa, false);
+    INF_TRY(launch_net313_multi(&f, 1, nx->fhid, MODE_EVALSAVE, s, 2));
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Y = bfa.Y;
+    a.y_sample = (long)nx->M3 * nx->P;
+    a.C = nx->C;
+    a.H = nx->H;
+    a.W = nx->W;
+    a.ks = 3;
+    a.mode = OM_EMBED;
+    a.bias = nx->L[2].b;
+    a.in0 = x;
+    a.out0 = bfa.fx;
+    a.out1 = bfa.xemb;
+    INF_TRY(launch_conv_out(a, B, s));
+  }
+  InfBroydenStats st;
+  INF_TRY(broyden_solve(nz, x, B, T, eps, &st, nullptr, bfa, s));
+  if (stats) *stats = st;
+  if (!st.prot_break) {
+    INF_TRY(glue_recomp(bfa.fx, bfa.flow, x, z, (long)B * nx->d, s));
+  } else {
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in0 = bfa.fx;
+    a.in1 = x;
+    a.out0 = z;
+    INF_TRY(run_forward(nz, bfa.lowest, B, bfa, OM_RECOMP, &a, s));
+  }
+  InfNet* nets[2] = {nx, nz};
+  const float* xs[2] = {x, z};
+  const float* es[2] = {eps_x, eps_z};
+  float* outs[2] = {logdet_x, logdet_z};
+  Bufs bfs[2] = {bfa, bfb};
+  return series_fused(nets, xs, es, 2, coeff, n_terms, outs, B, bfs, s, /*save_mask=*/2u);
 }
 
 int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,

@@ -12,6 +12,8 @@
 //   MODE_SAVE  forward, saving: A: d1 = swish'(a + b1)  B: d2 = swish'(a + b2)   (no phase C; the
 //              log-det estimator only needs the activation derivatives, implicit_block.py:318-319)
 //   MODE_VJP   v^T J          : A: (W3^T-flipped . v) * d2   B: (W2^T . t) * d1   C: taps of W1^T
+//   MODE_EVALSAVE  MODE_EVAL that also writes d1, d2 (x_embed pass of the x-net, whose log-det series
+//              needs the derivatives at the same input)
 // so one VJP of the series costs one launch that reads d1, d2 (the minimal HBM traffic) instead of
 // three GEMM launches that round-trip two HID-channel tensors through HBM.
 //
@@ -285,11 +287,11 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           } else {
             const float z = acc[m][b][r] + a.b1[o];
             v = swish_f(z, sp1);
-            if constexpr (MODE == MODE_SAVE) dv[r] = swish_d(z, sp1);
+            if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) dv[r] = swish_d(z, sp1);
           }
           t[o * F_BN + b * 32 + li] = v;
         }
-        if constexpr (MODE == MODE_SAVE) store_d(a.d1, m, b, dv);
+        if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) store_d(a.d1, m, b, dv);
       }
   }
   __syncthreads();
@@ -327,7 +329,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       tileB(kt + 1, a1);
     }
   }
-  if constexpr (MODE == MODE_SAVE) {
+  if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) {
     const float sp2 = softplus_f(*a.beta2);
 #pragma unroll
     for (int m = 0; m < TM; ++m)
@@ -338,6 +340,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int r = 0; r < 16; ++r) dv[r] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
         store_d(a.d2, m, b, dv);
       }
+  }
+  if constexpr (MODE == MODE_SAVE) {
     return;
   } else {
     // epilogue B -> t (after every wave finished reading t); VJP loads its multiplier d1 here (issuing it
@@ -348,7 +352,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) load_d(a.d1, m, b, dmul[m][b]);
     }
-    const float sp2 = (MODE == MODE_EVAL) ? softplus_f(*a.beta2) : 0.f;
+    const float sp2 = (MODE != MODE_VJP) ? softplus_f(*a.beta2) : 0.f;
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -490,7 +494,8 @@ int net313_supported(int hid, int C, int H, int W) {
 
 // Launch one or two nets (same shape) as one grid.  The 64-pixel tile is used unless the grid would
 // leave CUs idle (fewer than 256 workgroups), then 32-pixel tiles.
-int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s) {
+int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets) {
+  if (layout_nets <= 0) layout_nets = nnets;
   const Net313Args& a0 = args[0];
   if (!net313_supported(hid, a0.C, a0.H, a0.W) || nnets < 1 || nnets > 2) return INF_ERR_UNSUPPORTED;
   const int P = a0.H * a0.W;
@@ -502,7 +507,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // variant when neither fits
   const bool f64 = variant_fits(hid, a0.C, a0.H, a0.W, V64), fh = variant_fits(hid, a0.C, a0.H, a0.W, VHALF);
   int var = f64 ? V64 : (fh ? VHALF : VWIDE);
-  if (var == V64 && nnets * a0.B * (P / 64) < 256 && fh) var = VHALF;
+  if (var == V64 && layout_nets * a0.B * (P / 64) < 256 && fh) var = VHALF;
   if (force_bn == 64 && f64) var = V64;
   if (force_bn == 32 && fh) var = VHALF;
   static const int force_var = [] {
@@ -535,6 +540,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   do {                                                 \
     if (mode == MODE_EVAL) L313(TM_, MODE_EVAL, BN_);  \
     else if (mode == MODE_SAVE) L313(TM_, MODE_SAVE, BN_); \
+    else if (mode == MODE_EVALSAVE) L313(TM_, MODE_EVALSAVE, BN_); \
     else L313(TM_, MODE_VJP, BN_);                     \
   } while (0)
   if (hid == 512) L313M(2, bn);
@@ -547,6 +553,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     const double fA = 2.0 * hid * 9.0 * a0.C, fB = 2.0 * hid * hid;
     const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
     const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
+    // (EVALSAVE: x + d1/d2 writes + taps, the same expression)
     prof_end_launch(s, 500 + 10 * var + mode, npx * (fA + fB + fC), bytes);   // 50x / 51x (_h) / 52x (_w)
   }
   return INF_OK;

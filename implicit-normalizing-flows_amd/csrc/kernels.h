@@ -120,7 +120,7 @@ int launch_series_combine(const double* partials, const float* coeff_dev, int n_
 // ------------------------------------------------------------------------------------------
 // fused 3-1-3 conv net (fused313.hip): one launch per forward / derivative-saving forward / VJP
 // ------------------------------------------------------------------------------------------
-enum Net313Mode { MODE_EVAL = 0, MODE_SAVE = 1, MODE_VJP = 2 };
+enum Net313Mode { MODE_EVAL = 0, MODE_SAVE = 1, MODE_VJP = 2, MODE_EVALSAVE = 3 };
 struct Net313Args {
   const float* in;        // (B, C, H, W): x (forward) or v (VJP)
   const float* pre_beta;  // forward: swish preact on `in` (nullptr: none)
@@ -153,7 +153,9 @@ struct Net313Pair {
 };
 int net313_supported(int hid, int C, int H, int W);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
-int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s);
+// layout_nets (> 0) picks the tile variant as if that many nets shared the grid: launches that write
+// derivatives for a paired series must use the pair's variant (the d1/d2 layout depends on it)
+int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets = 0);
 
 // ------------------------------------------------------------------------------------------
 // opt-in launch timing (inf_profile_begin/end): hipEvents around every engine kernel launch,

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libinflow.so')
 
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
+INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
 
 
 class PowerIterDesc(ctypes.Structure):
@@ -72,6 +73,9 @@ _SIGS = {
     'inf_net_vjp': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_root_find': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                      ctypes.POINTER(BroydenStats), _P, _P, ctypes.c_size_t, _P]),
+    'inf_imblock_eval': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, _P,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(BroydenStats), _P,
+                                        ctypes.c_size_t, _P]),
     'inf_imblock_backward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                             ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_imblock_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
@@ -292,7 +296,7 @@ def profile_end():
 def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
     if 500 <= tag < 530:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide)
-        return 'net313_kernel%s<%s>' % (['', '_h', '_w'][(tag - 500) // 10], ['EVAL', 'SAVE', 'VJP'][tag % 10])
+        return 'net313_kernel%s<%s>' % (['', '_h', '_w'][(tag - 500) // 10], ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
     if tag < 1000:
         modes = {0: 'PLAIN', 1: 'EMBED', 2: 'RESID', 3: 'RECOMP', 4: 'VJP'}
         return 'conv_out_kernel<%d> mode %s' % (tag % 10, modes.get((tag - 900) // 10, '?'))

@@ -278,6 +278,10 @@ class imBlock(nn.Module):
                 self.nnet_x_copy(x)
                 self.nnet_z_copy(x)
         nx, nz, stream = self._native(x)
+        if logpx is not None and not self.training and not self.exact_trace and x.dim() == 4:
+            out = self._eval_fused(nx, nz, x, stream)
+            if out is not None:
+                return out[0], logpx - out[1]
         with torch.no_grad():
             z = self._root(nz, nx, x, self.eps_forward, stream, forward=True)
         if self.training:       # keep the frozen copies in step (implicit_block.py:228-229)
@@ -286,6 +290,33 @@ class imBlock(nn.Module):
         if logpx is None:
             return z
         return z, logpx - self._logdetgrad(z, x)
+
+    def _eval_fused(self, nx, nz, x, stream):
+        """Eval forward + log-det in one engine call (inf_imblock_eval) when both nets are fused.  The series
+        length and the probes are drawn first, in the reference's order (the forward draws nothing); if
+        the engine declines, the separate calls reuse the same draws.  Returns (z, logdet (B, 1))."""
+        lib = _hip.load()
+        x = x.contiguous()
+        B, T = x.shape[0], int(self.threshold)
+        plan = self._series_plan()
+        n_ps, coeff_fn, ns = plan
+        probes = (_probes(x.shape, x.device), _probes(x.shape, x.device))
+        co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+        ws = _hip.workspace(x.device, nx.ws_bytes(B, T) + nz.ws_bytes(B, 1))
+        z = torch.empty_like(x)
+        out = torch.empty(2, B, device=x.device)
+        st = _hip.BroydenStats()
+        rc = lib.inf_imblock_eval(nx.handle, nz.handle, _hip.ptr(x), _hip.ptr(z), _hip.ptr(probes[0]),
+                                  _hip.ptr(probes[1]), co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps,
+                                  _hip.ptr(out[0]), _hip.ptr(out[1]), B, T, float(self.eps_forward), ctypes.byref(st),
+                                  _hip.ptr(ws), ws.numel(), stream)
+        if rc == _hip.INF_ERR_UNSUPPORTED:
+            with torch.no_grad():
+                z = self._root(nz, nx, x, self.eps_forward, stream, forward=True)
+            return z, self._logdetgrad(z, x, plan=plan, probes=probes)
+        _hip.check(rc, 'inf_imblock_eval')
+        self.last_broyden = st.as_dict(T)
+        return z, self._finish_logdet(out[0] - out[1], n_ps, ns)
 
     def inverse(self, z, logpy=None):
         nx, nz, stream = self._native(z)
@@ -317,8 +348,9 @@ class imBlock(nn.Module):
         n_exact = self.n_exact_terms if self.training else self.n_exact_terms_test
         return solvers.series_coefficients(self.n_dist, param, n_exact, self.n_samples)
 
-    def _logdetgrad(self, z, x):
-        """log|det dz/dx| per sample, shape (B, 1) (implicit_block.py:245-350)."""
+    def _logdetgrad(self, z, x, plan=None, probes=None):
+        """log|det dz/dx| per sample, shape (B, 1) (implicit_block.py:245-350).  plan / probes: draws already
+        made by the caller (_eval_fused), in the reference's order."""
         lib = _hip.load()
         nx, nz, stream = self._native(x)
         B = x.shape[0]
@@ -329,15 +361,18 @@ class imBlock(nn.Module):
                 _hip.check(lib.inf_logdet_exact(net.handle, _hip.ptr(t.contiguous()), _hip.ptr(out[i]), B,
                                                 _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_exact')
             return (out[0] - out[1]).view(-1, 1)
-        n_ps, coeff_fn, ns = self._series_plan()
+        n_ps, coeff_fn, ns = plan if plan is not None else self._series_plan()
         if self.exact_trace:     # exact Jacobian traces, fc nets (implicit_block.py:323-343); no probes drawn
             if x.dim() != 2:
                 raise NotImplementedError('exact_trace=True needs the full Jacobian; supported for fc nets (d <= 16)')
             logdetgrad = (solvers.exact_trace_logdet(nx, x, n_ps, coeff_fn, stream) -
                           solvers.exact_trace_logdet(nz, z, n_ps, coeff_fn, stream))
             return self._finish_logdet(logdetgrad, n_ps, ns)
-        vareps_x = _probes(x.shape, x.device)
-        vareps_z = _probes(z.shape, z.device)
+        if probes is not None:
+            vareps_x, vareps_z = probes
+        else:
+            vareps_x = _probes(x.shape, x.device)
+            vareps_z = _probes(z.shape, z.device)
         ws = _hip.workspace(x.device, max(nx.ws_bytes(B), nz.ws_bytes(B)))
         out = torch.empty(2, B, device=x.device)
         if self.training and self.neumann_grad:

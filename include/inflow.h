@@ -121,6 +121,15 @@ int inf_logdet_series(InfNet* net, const float* x, const float* vareps, const fl
 int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_a, InfNet* net_b, const float* x_b,
                            const float* vareps_b, const float* coeff, int n_terms, float* out_a, float* out_b,
                            int batch, void* ws, size_t ws_bytes, void* stream);
+/* The whole eval pass of an imBlock whose two nets take the fused path (implicit_block.py:220-234 and the
+ * eval branch of 245-322): root solve, z = (f_x(x) - f_z(z*)) + x, and both power series with probes
+ * eps_x / eps_z and coeff[k-1] = (-1)^(k+1)/k coeff_fn(k); logdet_x[b], logdet_z[b] receive the two
+ * series (the block's log-det is their difference).  The x_embed pass also saves f_x's derivatives, so
+ * only the z-net needs its own.  INF_ERR_UNSUPPORTED when a net is not fused (use the separate calls).
+ * ws >= inf_workspace_bytes(net_x, batch, threshold) + inf_workspace_bytes(net_z, batch, 1). */
+int inf_imblock_eval(InfNet* net_x, InfNet* net_z, const float* x, float* z, const float* eps_x, const float* eps_z,
+                     const float* coeff, int n_terms, float* logdet_x, float* logdet_z, int batch, int threshold,
+                     double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
 /* Neumann gradient surrogate value (implicit_block.py:429-438): w = sum_{k=0}^{n} ncoeff[k] (J^T)^k eps,
  * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
 int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,
