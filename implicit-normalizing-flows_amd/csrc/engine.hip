@@ -568,6 +568,165 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   return INF_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Parameter gradients (training path) on the generic GEMM operands (W_eff packed at refresh).
+// Conv nets whose intermediate activations are swish: layer l computes h_l = W_l * in_l + b_l,
+// in_0 = preact(x), in_l = swish(h_{l-1}) (applied on load from the stored pre-activation).
+// ---------------------------------------------------------------------------------------------
+struct GradBufs {
+  std::vector<float*> H, Hd, Ad;     // pre-activations, their tangents, activation tangents (Ad[0]: input)
+  float *gA, *gB, *hA, *hB, *gad, *ga, *Y, *slab, *dWe, *dWe2, *dsig, *xin, *tmp_in;
+  double *bpart, *dot;
+  int max_split;
+};
+constexpr int GRAD_SPLIT = 32;
+constexpr int GRAD_BLOCKS = 512;
+
+size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
+  WS w{reinterpret_cast<char*>(ws), cap, 0};
+  const size_t hid = (size_t)B * n->hidden_max * n->P, in = (size_t)B * n->d;
+  const int L = (int)n->L.size();
+  size_t mn = 1;
+  for (const auto& l : n->L) mn = std::max(mn, (size_t)l.cout * l.cin * l.ks * l.ks);
+  g.H.resize(L > 0 ? L - 1 : 0);
+  g.Hd.resize(L > 0 ? L - 1 : 0);
+  g.Ad.resize(L > 0 ? L : 0);
+  for (auto& p : g.H) p = w.take<float>(hid);
+  for (auto& p : g.Hd) p = w.take<float>(hid);
+  for (int l = 0; l < L; ++l) g.Ad[l] = w.take<float>(l == 0 ? in : hid);
+  for (float** p : {&g.gA, &g.gB, &g.hA, &g.hB, &g.gad, &g.ga}) *p = w.take<float>(std::max(hid, in));
+  g.Y = w.take<float>((size_t)B * n->rows_max * n->P);
+  g.slab = w.take<float>((size_t)GRAD_SPLIT * mn);
+  g.dWe = w.take<float>(mn);
+  g.dWe2 = w.take<float>(mn);
+  g.dsig = w.take<float>(mn);
+  g.xin = w.take<float>(in);
+  g.tmp_in = w.take<float>(in);
+  g.bpart = w.take<double>(GRAD_BLOCKS + 64);
+  g.dot = w.take<double>(64);
+  g.max_split = GRAD_SPLIT;
+  return w.off + 256;
+}
+
+// h_l = W_l * in (+ b_l); in gets swish(., pre_beta) on load when pre_beta is set.  l < L-1 (no taps).
+static int layer_fwd(InfNet* n, int l, const float* in, const float* pre_beta, bool bias, float* out, int B,
+                     hipStream_t s) {
+  const WLayer& w = n->L[l];
+  GemmArgs g = gemm_base(n, w.f, in, w.cin, B);
+  g.pre_beta = pre_beta;
+  set_out(n, g, out, w.cout);
+  g.bias = bias ? w.b : nullptr;
+  return launch_gemm(g, w.f.load, bias ? EP_BIAS : EP_STORE, s);
+}
+
+// out = W_l^T gout  (input-side gradient of layer l, no activation factor)
+static int layer_vjp(InfNet* n, int l, const float* gout, float* out, int B, GradBufs& gb, hipStream_t s) {
+  const WLayer& w = n->L[l];
+  GemmArgs g = gemm_base(n, w.g, gout, w.cout, B);
+  if (w.g.taps) {
+    set_out(n, g, gb.Y, w.g.M);
+    INF_TRY(launch_gemm(g, w.g.load, EP_STORE, s));
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Y = gb.Y;
+    a.y_sample = (long)w.g.M * n->P;
+    a.C = w.cin;
+    a.H = n->H;
+    a.W = n->W;
+    a.ks = 3;
+    a.mode = OM_VJP;
+    a.out0 = out;
+    return launch_conv_out(a, B, s);
+  }
+  set_out(n, g, out, w.cin);
+  return launch_gemm(g, w.g.load, EP_STORE, s);
+}
+
+// dW_eff of layer l = sum_{b,p} G (x) X~ (accumulate: add into gb.dWe), X = in_l
+static int layer_wgrad(InfNet* n, int l, const float* G, const float* X, const float* x_beta, float* out, int B,
+                       GradBufs& gb, hipStream_t s) {
+  const WLayer& w = n->L[l];
+  WgradArgs a;
+  memset(&a, 0, sizeof(a));
+  a.G = G;
+  a.g_sample = (long)w.cout * n->P;
+  a.X = X;
+  a.x_sample = (long)w.cin * n->P;
+  a.x_beta = x_beta;
+  a.B = B;
+  a.P = n->P;
+  a.H = n->H;
+  a.W = n->W;
+  a.ks = w.ks;
+  a.M = w.cout;
+  a.N = w.cin * w.ks * w.ks;
+  a.slab = gb.slab;
+  a.out = out;
+  a.max_split = gb.max_split;
+  return launch_wgrad(a, s);
+}
+
+// dW (raw weight) from dW_eff through W_eff = W / max(1, sigma / coeff), sigma = u . (W v)
+static int layer_sigma_chain(InfNet* n, int l, const float* dWe, float* dW, GradBufs& gb, hipStream_t s) {
+  const WLayer& w = n->L[l];
+  const bool spatial = w.ks > 1;
+  WgradArgs a;                                  // dsigma/dW = u (x) v~ (one "sample")
+  memset(&a, 0, sizeof(a));
+  a.G = w.u;
+  a.X = w.v;
+  a.B = 1;
+  a.P = spatial ? n->P : 1;
+  a.H = spatial ? n->H : 1;
+  a.W = spatial ? n->W : 1;
+  a.g_sample = (long)w.cout * a.P;
+  a.x_sample = (long)w.cin * a.P;
+  a.ks = w.ks;
+  a.M = w.cout;
+  a.N = w.cin * w.ks * w.ks;
+  a.slab = gb.slab;
+  a.out = gb.dsig;
+  a.max_split = gb.max_split;
+  INF_TRY(launch_wgrad(a, s));
+  return launch_sigma_chain(dWe, w.W, gb.dsig, w.factor, w.coeff, gb.dot, dW, (long)w.cout * w.cin * w.ks * w.ks, s);
+}
+
+static bool grad_supported(const InfNet* n) {
+  if (n->fc || n->L.empty()) return false;
+  for (size_t l = 0; l + 1 < n->L.size(); ++l)
+    if (n->L[l].act != ACT_SWISH) return false;
+  if (n->L.back().act != ACT_NONE) return false;
+  return n->pre_act == ACT_NONE || n->pre_act == ACT_SWISH;
+}
+
+static float* grad_out(float* const* arr, int l) { return arr ? arr[l] : nullptr; }
+
+// layer l's gradients from G_hd (against the tangent input) and G_h (against the primal input, may be null)
+static int layer_param_grads(InfNet* n, int l, const float* G_tan, const float* X_tan, const float* G_pri,
+                             const float* X_pri, const float* X_pri_beta, const InfNetGrads* gr, int B, GradBufs& gb,
+                             hipStream_t s) {
+  const WLayer& w = n->L[l];
+  float* dW = grad_out(gr->dW, l);
+  if (dW) {
+    const long mn = (long)w.cout * w.cin * w.ks * w.ks;
+    if (G_tan) {
+      INF_TRY(layer_wgrad(n, l, G_tan, X_tan, nullptr, gb.dWe, B, gb, s));
+      if (G_pri) {
+        INF_TRY(layer_wgrad(n, l, G_pri, X_pri, X_pri_beta, gb.dWe2, B, gb, s));
+        INF_TRY(glue_add(gb.dWe2, gb.dWe, gb.dWe, mn, s));
+      }
+    } else {
+      INF_TRY(layer_wgrad(n, l, G_pri, X_pri, X_pri_beta, gb.dWe, B, gb, s));
+    }
+    INF_TRY(layer_sigma_chain(n, l, gb.dWe, dW, gb, s));
+  }
+  float* db = grad_out(gr->db, l);
+  if (db) {
+    if (G_pri) INF_TRY(launch_channel_sum(G_pri, B, w.cout, n->P, db, s));
+    else INF_HIP(hipMemsetAsync(db, 0, sizeof(float) * w.cout, s));
+  }
+  return INF_OK;
+}
+
 }  // namespace
 
 // ==============================================================================================
@@ -1296,6 +1455,134 @@ int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* s
   if (!out && n) return INF_ERR_INVALID;
   return glue_rademacher(out, n, seed, offset, (hipStream_t)stream);
 }
+// Gradient of sum(gout * f(x)) with respect to every parameter of a conv net (and x): the recompute
+// graph of the training forward (implicit_block.py:226-227) and the first-order terms of any caller.
+int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, const InfNetGrads* gr, int B,
+                       void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !gout || !gr || B <= 0) return INF_ERR_INVALID;
+  if (!grad_supported(n)) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  GradBufs gb;
+  if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
+  const int L = (int)n->L.size();
+  const long hidP = (long)n->P;
+  // forward: pre-activations
+  for (int l = 0; l + 1 < L; ++l) {
+    const float* in = l == 0 ? x : gb.H[l - 1];
+    const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+    INF_TRY(layer_fwd(n, l, in, pb, true, gb.H[l], B, s));
+  }
+  // backward
+  const float* g = gout;
+  float* bufs[2] = {gb.gA, gb.gB};
+  for (int l = L - 1; l >= 0; --l) {
+    const float* X = l == 0 ? x : gb.H[l - 1];
+    const float* xb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+    INF_TRY(layer_param_grads(n, l, nullptr, nullptr, g, X, xb, gr, B, gb, s));
+    if (l > 0) {
+      const WLayer& prev = n->L[l - 1];
+      const long ne = (long)B * prev.cout * hidP;
+      INF_TRY(layer_vjp(n, l, g, gb.ga, B, gb, s));
+      float* gp = bufs[l & 1];
+      INF_TRY(launch_act_bwd1(gb.ga, gb.H[l - 1], prev.act_beta, gp, gb.bpart, ne, GRAD_BLOCKS, s));
+      float* dbeta = grad_out(gr->dbeta, l - 1);
+      if (dbeta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
+      g = gp;
+    } else if (gx || (n->pre_beta && gr->dpre_beta)) {
+      const long ne = (long)B * n->d;
+      float* gin = gx ? gx : gb.tmp_in;
+      if (n->pre_beta) {
+        INF_TRY(layer_vjp(n, 0, g, gb.ga, B, gb, s));
+        INF_TRY(launch_act_bwd1(gb.ga, x, n->pre_beta, gin, gb.bpart, ne, GRAD_BLOCKS, s));
+        if (gr->dpre_beta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, gr->dpre_beta, 0, s));
+      } else {
+        INF_TRY(layer_vjp(n, 0, g, gin, B, gb, s));
+      }
+    }
+  }
+  return INF_OK;
+}
+
+// Gradient of s = sum_b w_b^T J(x_b) eps_b (w fixed) with respect to x and every parameter, and the value
+// s_b per sample: the memory-efficient Neumann estimator's surrogate (implicit_block.py:388-394,437-438),
+// forward-over-reverse on the engine.
+int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const float* eps, float* value, float* gx,
+                           const InfNetGrads* gr, int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !w || !eps || !gr || B <= 0) return INF_ERR_INVALID;
+  if (!grad_supported(n)) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  GradBufs gb;
+  if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
+  const int L = (int)n->L.size();
+  const long nin = (long)B * n->d;
+  // input tangent: eps * preact'(x) (or eps)
+  const float* in_tan = eps;
+  if (n->pre_beta) {
+    INF_HIP(hipMemcpyAsync(gb.Ad[0], eps, sizeof(float) * nin, hipMemcpyDeviceToDevice, s));
+    INF_TRY(launch_act_tangent(gb.Ad[0], x, n->pre_beta, nin, s));
+    in_tan = gb.Ad[0];
+  }
+  // forward: primal pre-activations H, tangents Hd, activation tangents Ad
+  for (int l = 0; l + 1 < L; ++l) {
+    const float* in = l == 0 ? x : gb.H[l - 1];
+    const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+    INF_TRY(layer_fwd(n, l, in, pb, true, gb.H[l], B, s));
+    const float* tin = l == 0 ? in_tan : gb.Ad[l];
+    INF_TRY(layer_fwd(n, l, tin, nullptr, false, gb.Hd[l], B, s));
+    const long ne = (long)B * n->L[l].cout * n->P;
+    INF_HIP(hipMemcpyAsync(gb.Ad[l + 1], gb.Hd[l], sizeof(float) * ne, hipMemcpyDeviceToDevice, s));
+    INF_TRY(launch_act_tangent(gb.Ad[l + 1], gb.H[l], n->L[l].act_beta, ne, s));
+  }
+  // reverse: G_tan = gbar of the layer's tangent output, G_pri = gbar of its primal output
+  const float* G_tan = w;
+  const float* G_pri = nullptr;
+  float* tb[2] = {gb.gA, gb.gB};
+  float* pb2[2] = {gb.hA, gb.hB};
+  for (int l = L - 1; l >= 0; --l) {
+    const float* X_tan = l == 0 ? in_tan : gb.Ad[l];
+    const float* X_pri = l == 0 ? x : gb.H[l - 1];
+    const float* xb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+    INF_TRY(layer_param_grads(n, l, G_tan, X_tan, G_pri, X_pri, xb, gr, B, gb, s));
+    INF_TRY(layer_vjp(n, l, G_tan, gb.gad, B, gb, s));
+    if (G_pri) INF_TRY(layer_vjp(n, l, G_pri, gb.ga, B, gb, s));
+    if (l == L - 1 && value) {
+      // s_b = sum w . (W_{L-1} * adot_{L-2}) = sum (W_{L-1}^T w) . adot_{L-2}
+      const long per = (long)n->L[l].cin * n->P;
+      INF_TRY(glue_batched_dot(gb.gad, X_tan, value, B, per, s));
+    }
+    if (l > 0) {
+      const WLayer& prev = n->L[l - 1];
+      const long ne = (long)B * prev.cout * n->P;
+      float* nt = tb[l & 1];
+      float* np = pb2[l & 1];
+      INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, gb.H[l - 1], gb.Hd[l - 1], prev.act_beta, nt, np,
+                              gb.bpart, ne, GRAD_BLOCKS, s));
+      float* dbeta = grad_out(gr->dbeta, l - 1);
+      if (dbeta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
+      G_tan = nt;
+      G_pri = np;
+    } else {
+      float* gin = gx ? gx : gb.tmp_in;
+      if (n->pre_beta) {
+        // x-gradient: gbar_adot eps s''(x) + gbar_a s'(x); beta: ... (act_bwd2 with h = x, hdot = eps)
+        INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, x, eps, n->pre_beta, gb.xin, gin, gb.bpart, nin,
+                                GRAD_BLOCKS, s));
+        if (gr->dpre_beta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, gr->dpre_beta, 0, s));
+      } else if (gx) {
+        if (G_pri) INF_HIP(hipMemcpyAsync(gx, gb.ga, sizeof(float) * nin, hipMemcpyDeviceToDevice, s));
+        else INF_HIP(hipMemsetAsync(gx, 0, sizeof(float) * nin, s));
+      }
+    }
+  }
+  return INF_OK;
+}
+
+size_t inf_grad_workspace_bytes(InfNet* n, int B) {
+  if (!n || B <= 0) return 0;
+  GradBufs gb;
+  return carve_grad(n, B, nullptr, 0, gb);
+}
+
 int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
 
 }  // extern "C"

@@ -186,6 +186,21 @@ int glue_recomp(const float* fx, const float* fz, const float* x, float* out, lo
   return INF_OK;
 }
 
+// out[b] = sum_i a[b][i] * c[b][i]  (fp64, one workgroup per sample)
+__global__ __launch_bounds__(256) void batched_dot_kernel(const float* a, const float* c, float* out, long per) {
+  __shared__ double red[16];
+  const long base = (long)blockIdx.x * per;
+  double acc = 0.0;
+  for (long i = threadIdx.x; i < per; i += blockDim.x) acc += (double)a[base + i] * (double)c[base + i];
+  const double t = block_sum(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)t;
+}
+int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, hipStream_t s) {
+  hipLaunchKernelGGL(batched_dot_kernel, dim3(B), dim3(256), 0, s, a, c, out, per);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // 160 KiB of LDS per workgroup, one workgroup per CU at a time; 8 waves of 4 per CU cover every CU.
 __global__ __launch_bounds__(1024) void poison_lds_kernel(float* sink) {
   __shared__ float lds[40960];

@@ -158,6 +158,32 @@ int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets = 0);
 
 // ------------------------------------------------------------------------------------------
+// parameter gradients (grad.hip)
+// ------------------------------------------------------------------------------------------
+struct WgradArgs {
+  const float* G;         // (B, M, P) output gradient
+  long g_sample;
+  const float* X;         // (B, Cin, P) layer input (or a pre-activation with x_beta)
+  long x_sample;
+  const float* x_beta;    // non-null: X <- swish(X) on load (stored pre-activation of the previous layer)
+  int B, P, H, W, ks;     // ks = 1 or 3 (pad ks/2)
+  int M, N;               // M = cout, N = cin * ks * ks
+  float* slab;            // nsplit * M * N floats
+  float* out;             // M * N
+  int nsplit, max_split;
+};
+int launch_wgrad(const WgradArgs& a, hipStream_t s);
+int launch_act_bwd1(const float* ga, const float* h, const float* beta, float* gprev, double* bpart, long n,
+                    int nblocks, hipStream_t s);
+int launch_act_tangent(float* hdot, const float* h, const float* beta, long n, hipStream_t s);
+int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, const float* beta,
+                    float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks, hipStream_t s);
+int launch_channel_sum(const float* g, int B, int C, int P, float* out, hipStream_t s);
+int launch_beta_reduce(const double* bpart, int n, float* out, int accumulate, hipStream_t s);
+int launch_sigma_chain(const float* dWe, const float* W, const float* dsig, const float* factor, float coeff,
+                       double* dot, float* dW, long n, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
 // opt-in launch timing (inf_profile_begin/end): hipEvents around every engine kernel launch,
 // tagged with the kernel instantiation and its algorithmic FLOPs / bytes.  Off by default; a
 // debug/measurement facility, not re-entrant.

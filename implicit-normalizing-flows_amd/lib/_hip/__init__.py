@@ -25,6 +25,11 @@ class PowerIterDesc(ctypes.Structure):
                 ('u', ctypes.c_void_p), ('v', ctypes.c_void_p), ('scale', ctypes.c_void_p)]
 
 
+class NetGrads(ctypes.Structure):
+    _fields_ = [('dW', ctypes.POINTER(ctypes.c_void_p)), ('db', ctypes.POINTER(ctypes.c_void_p)),
+                ('dbeta', ctypes.POINTER(ctypes.c_void_p)), ('dpre_beta', ctypes.c_void_p)]
+
+
 class LayerDesc(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int), ('cin', ctypes.c_int), ('cout', ctypes.c_int), ('ksize', ctypes.c_int),
                 ('weight', ctypes.c_void_p), ('bias', ctypes.c_void_p), ('u', ctypes.c_void_p),
@@ -102,6 +107,11 @@ _SIGS = {
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
+    'inf_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int]),
+    'inf_net_param_grad': (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t,
+                                          _P]),
+    'inf_net_surrogate_grad': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P,
+                                              ctypes.c_size_t, _P]),
     'inf_power_iteration_workspace_bytes': (ctypes.c_size_t, [ctypes.POINTER(PowerIterDesc)]),
     'inf_power_iteration': (ctypes.c_int, [ctypes.POINTER(PowerIterDesc), ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                            ctypes.c_float, ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),

@@ -198,6 +198,27 @@ size_t inf_power_iteration_workspace_bytes(const InfPowerIterDesc* desc);
 int inf_power_iteration(const InfPowerIterDesc* desc, int max_iters, int use_tol, float atol, float rtol,
                         int* iters_used, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- parameter gradients (training path; conv nets with swish activations) ------------------------
+ * Device buffers per weight layer l (in order; NULL entries / arrays are skipped): dW[l] the gradient of
+ * the RAW weight (through W / max(1, u.(W v) / coeff), mixed_lipschitz.py:378-385), db[l] the bias,
+ * dbeta[l] the beta of the swish applied after layer l (NULL for the last layer); dpre_beta the
+ * preact swish.  Buffers are overwritten. */
+typedef struct InfNetGrads {
+  float** dW;
+  float** db;
+  float** dbeta;
+  float* dpre_beta;
+} InfNetGrads;
+size_t inf_grad_workspace_bytes(InfNet* net, int batch);
+/* d/dtheta sum(gout * nnet(x)) and d/dx (gx may be NULL): the recompute graph's backward
+ * (z = f_x(x0) - f_z(z*) + x0, implicit_block.py:226-227). */
+int inf_net_param_grad(InfNet* net, const float* x, const float* gout, float* gx, const InfNetGrads* grads,
+                       int batch, void* ws, size_t ws_bytes, void* stream);
+/* s_b = w_b^T J(x_b) eps_b (w fixed): value[b] (may be NULL) and d/dx, d/dtheta of sum_b s_b -- the
+ * memory-efficient Neumann estimator's surrogate and its gradients (implicit_block.py:388-394,437-438). */
+int inf_net_surrogate_grad(InfNet* net, const float* x, const float* w, const float* eps, float* value, float* gx,
+                           const InfNetGrads* grads, int batch, void* ws, size_t ws_bytes, void* stream);
+
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);

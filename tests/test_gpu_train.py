@@ -123,3 +123,64 @@ def test_iresblock_training_gradients_match_reference(golden_dir, name, neumann,
     loss.backward()
     assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
     assert _check_grads(blk, g) == len([k for k in g.files if k.startswith('g:')])
+
+
+def _conv_net(C, hid, preact):
+    from lib.layers.base import InducedNormConv2d, Swish
+    conv = lambda a, b, k: InducedNormConv2d(a, b, k, 1, k // 2, coeff=0.9, atol=1e-3, rtol=1e-3)
+    mods = ([Swish()] if preact else []) + [conv(C, hid, 3), Swish(), conv(hid, hid, 1), Swish(), conv(hid, C, 3)]
+    return torch.nn.Sequential(*mods)
+
+
+def _check_param(got, ref, name, rel=2e-4):
+    scale = max(ref.abs().max().item(), 1e-12)
+    err = (got - ref).abs().max().item()
+    assert err <= rel * scale + 1e-9, '%s: max err %g vs scale %g' % (name, err, scale)
+
+
+@pytest.mark.parametrize('C,hid,preact,H', [(3, 64, False, 16), (12, 64, True, 8), (3, 512, True, 32)])
+def test_engine_param_and_surrogate_grads_match_autograd(C, hid, preact, H):
+    """inf_net_param_grad / inf_net_surrogate_grad against torch autograd through the same modules
+    (compute_weight(update=False) keeps the Lipschitz normalisation in the graph)."""
+    from lib import _hip
+    from lib.layers import netgrad
+    torch.manual_seed(1)
+    net = _conv_net(C, hid, preact).to(DEV)
+    with torch.no_grad():
+        net(torch.zeros(1, C, H, H, device=DEV))
+        for m in net:
+            if hasattr(m, 'beta'):
+                m.beta.fill_(0.4)
+            if hasattr(m, 'weight'):
+                m.weight.mul_(3.0)               # sigma / coeff > 1: the normalisation is active
+        for m in net:
+            if hasattr(m, 'weight'):
+                m.compute_weight(update=True)
+    B = 2
+    x = (torch.randn(B, C, H, H) * 0.5).to(DEV)
+    gout = torch.randn(B, C, H, H).to(DEV)
+    w = torch.randn(B, C, H, H).to(DEV)
+    eps = torch.randn(B, C, H, H).sign().to(DEV)
+    params = list(net.parameters())
+    native = _hip.native_net(net, (C, H, H), x.device)
+    native.refresh_if_needed(_hip.stream_of(x))
+    # first order
+    xg = x.clone().requires_grad_(True)
+    ref = torch.autograd.grad((net(xg) * gout).sum(), params + [xg])
+    grads, gx = netgrad.param_grads(native, net, x, gout, want_x=True)
+    torch.cuda.synchronize()
+    for p, r in zip(params, ref[:-1]):
+        _check_param(grads[p], r, 'param %s' % (tuple(p.shape),))
+    _check_param(gx, ref[-1], 'x')
+    # surrogate (second order)
+    xg = x.clone().requires_grad_(True)
+    vjp = torch.autograd.grad(net(xg), xg, w, create_graph=True)[0]
+    s = torch.sum(vjp.view(B, -1) * eps.view(B, -1), 1)
+    ref2 = torch.autograd.grad(s.sum(), params + [xg], allow_unused=True)
+    value, grads2, gx2 = netgrad.surrogate_grads(native, net, x, w, eps)
+    torch.cuda.synchronize()
+    _check_param(value, s.detach(), 'value', rel=1e-5)
+    for p, r in zip(params, ref2[:-1]):
+        r = torch.zeros_like(p) if r is None else r
+        _check_param(grads2[p], r, 'surrogate param %s' % (tuple(p.shape),))
+    _check_param(gx2, ref2[-1], 'surrogate x')
