@@ -18,8 +18,10 @@ generator in the reference's order (vareps_x, then vareps_z), so seeded runs rep
 
 When a gradient is needed (training), the forward builds the reference's graph: the root solve and
 the n-term Neumann series run on the engine, the implicit backward (imBlock.Backward) is an engine
-Broyden solve over VJPs (inf_imblock_backward), and the once-per-step parameter-gradient
-bookkeeping (recompute graph, the surrogate's double backward) goes through autograd on the nets.
+Broyden solve over VJPs (inf_imblock_backward), and for conv nets with swish activations the
+parameter gradients too (inf_net_param_grad for the recompute graph, inf_net_surrogate_grad for the
+memory-efficient Neumann estimator).  Other nets (the fc tabular / toy nets) keep autograd on the
+nets for those two once-per-step pieces.
 """
 import copy
 import ctypes
@@ -29,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import _hip
-from . import solvers
+from . import netgrad, solvers
 
 __all__ = ['imBlock', 'set_probe_mode']
 
@@ -103,6 +105,50 @@ class _MemEffLogDet(torch.autograd.Function):
         it = iter(saved)
         grads = [None if none else next(it) * dL for none in ctx.none_mask]
         return (None, grad_x * dL) + tuple(grads)
+
+
+class _Recompute(torch.autograd.Function):
+    """z = (f_x(x0) - f_z(z*)) + x0 with x0, z* constants (implicit_block.py:226-227): the values come from
+    the engine's forward, the parameter gradients from inf_net_param_grad (d/dtheta_x of grad . f_x(x0),
+    minus d/dtheta_z of grad . f_z(z*))."""
+
+    @staticmethod
+    def forward(ctx, x0, z_star, blk, nx, nz, n_px, *params):
+        fx = blk._net_forward(nx, x0)
+        fz = blk._net_forward(nz, z_star)
+        ctx.save_for_backward(x0, z_star)
+        ctx.blk, ctx.nx, ctx.nz, ctx.n_px = blk, nx, nz, n_px
+        return (fx - fz) + x0
+
+    @staticmethod
+    def backward(ctx, grad):
+        x0, z_star = ctx.saved_tensors
+        blk = ctx.blk
+        gx, _ = netgrad.param_grads(ctx.nx, blk.nnet_x, x0, grad.contiguous())
+        gz, _ = netgrad.param_grads(ctx.nz, blk.nnet_z, z_star, (-grad).contiguous())
+        px = list(blk.nnet_x.parameters())
+        pz = list(blk.nnet_z.parameters())
+        out = [gx.get(p) for p in px] + [gz.get(p) for p in pz]
+        return (None, None, None, None, None, None) + tuple(out)
+
+
+class _MemEffNeumannNative(torch.autograd.Function):
+    """MemoryEfficientLogDetEstimator with the Neumann estimator, all on the engine: w from
+    inf_neumann_vector (outside), then the surrogate w^T J eps with its x- and parameter gradients from
+    inf_net_surrogate_grad; backward scales them by dL[0] (implicit_block.py:396-415)."""
+
+    @staticmethod
+    def forward(ctx, x, native, module, w, eps, *params):
+        value, grads, gx = netgrad.surrogate_grads(native, module, x.detach(), w, eps)
+        ctx.grads = [grads.get(p) for p in params]
+        ctx.save_for_backward(gx)
+        return value
+
+    @staticmethod
+    def backward(ctx, grad_ld):
+        gx, = ctx.saved_tensors
+        dL = grad_ld[0].detach()
+        return (gx * dL, None, None, None, None) + tuple(g * dL if g is not None else None for g in ctx.grads)
 
 
 def _needs_graph(module, *ts):
@@ -182,7 +228,11 @@ class imBlock(nn.Module):
         nx, nz, stream = self._native(x0)
         with torch.no_grad():
             z_star = self._root(nz, nx, x0, self.eps_forward, stream, forward=False)
-        z = (self.nnet_x(x0) - self.nnet_z(z_star)) + x0
+        if self._engine_grads(x0):
+            params = list(self.nnet_x.parameters()) + list(self.nnet_z.parameters())
+            z = _Recompute.apply(x0, z_star, self, nx, nz, len(list(self.nnet_x.parameters())), *params)
+        else:
+            z = (self.nnet_x(x0) - self.nnet_z(z_star)) + x0
         if self.training:
             self.nnet_x_copy.load_state_dict(self.nnet_x.state_dict())
             self.nnet_z_copy.load_state_dict(self.nnet_z.state_dict())
@@ -221,7 +271,12 @@ class imBlock(nn.Module):
         neumann = self.training and self.neumann_grad
         nx, nz, stream = self._native(x)
         ests = []
+        engine = self._engine_grads(x)
         for net, native, t, eps in ((self.nnet_x, nx, x, vareps_x), (self.nnet_z, nz, z, vareps_z)):
+            if neumann and engine and self.training and self.grad_in_forward:
+                w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
+                ests.append(_MemEffNeumannNative.apply(t, native, net, w, eps, *list(net.parameters())))
+                continue
             if neumann:
                 w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
                 est = (lambda net_, w_, eps_: lambda tg: solvers.surrogate_wJe(net_, tg, w_, eps_))(net, w, eps)
@@ -235,6 +290,32 @@ class imBlock(nn.Module):
                 with torch.enable_grad():
                     ests.append(est(tg))
         return self._finish_logdet(ests[0] - ests[1], n_ps, ns)
+
+    def _engine_grads(self, t):
+        """Whether the engine computes the parameter gradients of both nets (conv nets with swish
+        activations); otherwise the training graph keeps autograd on the nets."""
+        if t.dim() != 4:
+            return False
+        key = '_engine_grads_ok'
+        if key not in self.__dict__:
+            ok = True
+            for net in (self.nnet_x, self.nnet_z):
+                for m in net.modules():
+                    if isinstance(m, nn.Sequential):
+                        continue
+                    name = type(m).__name__
+                    if name not in ('InducedNormConv2d', 'Swish'):
+                        ok = False
+            self.__dict__[key] = ok
+        return self.__dict__[key]
+
+    def _net_forward(self, native, t):
+        B = t.shape[0]
+        ws = _hip.workspace(t.device, native.ws_bytes(B))
+        y = torch.empty_like(t)
+        _hip.check(_hip.load().inf_net_forward(native.handle, _hip.ptr(t.contiguous()), _hip.ptr(y), B, _hip.ptr(ws),
+                                               ws.numel(), _hip.stream_of(t)), 'inf_net_forward')
+        return y
 
     def _neumann_vector(self, native, t, eps, n_ps, coeff_fn, stream):
         B = t.shape[0]

@@ -91,6 +91,8 @@ def test_training_gradients_match_reference(golden_dir, name, arch):
         if arch['kind'] == 'conv':
             assert b.last_broyden_backward['nstep'] == int(g['b%d_bwd_nstep' % i]), 'block %d bwd nstep' % i
     assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
+    if arch['kind'] == 'conv':       # the engine computed the parameter gradients (no autograd on the nets)
+        assert all(b.__dict__.get('_engine_grads_ok') for b in blocks)
     n = _check_grads(m, g)
     assert n == len([k for k in g.files if k.startswith('g:') or k.startswith('gs:')])
 
