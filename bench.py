@@ -33,7 +33,7 @@ import torch  # noqa: E402
 
 from lib import _hip, distributed as dd, synthetic as syn  # noqa: E402
 from lib.configs import build_flow, imblocks  # noqa: E402
-from lib.density import image_logpx  # noqa: E402
+from lib.density import image_bits_per_dim_graph, image_logpx  # noqa: E402
 from lib.layers import set_probe_mode  # noqa: E402
 
 METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs are labelled alike
@@ -55,6 +55,9 @@ def parse():
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
     ap.add_argument('--cpu-batch', type=int, default=2)
+    ap.add_argument('--mode', default='eval', choices=['eval', 'train'],
+                    help='eval: the density-evaluation hot path (BASELINE metric); train: one training step '
+                         '(train-mode forward + loss.backward(), train_img.py:611-638; no optimizer step)')
     return ap.parse_args()
 
 
@@ -102,7 +105,20 @@ def main():
     np.random.seed(0)
     torch.manual_seed(0)
 
+    if args.mode == 'train':
+        model.train()
+        set_probe_mode('reference')           # the reference's train-mode probes (host generator)
+        params = [p for p in model.parameters() if p.requires_grad]
+
     def step(i):
+        if args.mode == 'train':
+            for p in params:
+                p.grad = None
+            bpd, logpx, _ = image_bits_per_dim_graph(model, xs[i % xs.shape[0]], arch['nvals'])
+            bpd.backward()
+            if world > 1:                      # data-parallel gradient all-reduce (one flat bucket)
+                dd.allreduce_grads(params)
+            return bpd.detach()
         _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
         s, n = dd.global_logpx_sum(logpx)      # the one collective per batch
         return dd.bits_per_dim(s, n, ndim)
@@ -146,8 +162,11 @@ def main():
         except Exception:
             traffic = None
 
+    if torch.is_tensor(bpd):
+        bpd = float(bpd)
     out = {
-        'metric': METRIC[args.config],
+        'metric': METRIC[args.config] if args.mode == 'eval' else
+        'samples/sec (whole node), %s training step (forward + backward)' % args.config,
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
@@ -172,7 +191,7 @@ def main():
                                     for s in stats], key=lambda r: -r['ms'])[:8]},
         'cpu_baseline': None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline and args.config != 'celebahq256':
+    if rank == 0 and world == 1 and args.cpu_baseline and args.config != 'celebahq256' and args.mode == 'eval':
         cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch)
         out['cpu_baseline'] = cb
         out['bpd_delta_vs_oracle'] = delta

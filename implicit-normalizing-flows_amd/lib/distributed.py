@@ -66,3 +66,21 @@ def max_over_ranks(value, device):
 def barrier():
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
+
+
+def allreduce_grads(params):
+    """Data-parallel training: average the gradients over ranks with ONE all-reduce of a flat bucket
+    (≈ 22 MB for the CIFAR model) instead of DataParallel's per-forward parameter broadcast."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    flat.div_(dist.get_world_size())
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
