@@ -602,8 +602,8 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
   g.dsig = w.take<float>(mn);
   g.xin = w.take<float>(in);
   g.tmp_in = w.take<float>(in);
-  g.bpart = w.take<double>(GRAD_BLOCKS + 64);
-  g.dot = w.take<double>(64);
+  g.bpart = w.take<double>(std::max<size_t>(GRAD_BLOCKS + 64, glue_batched_dot_scratch(B, (long)n->hidden_max * n->P) + 64));
+  g.dot = w.take<double>(128);      // [0] the dot, [1..64] its block partials
   g.max_split = GRAD_SPLIT;
   return w.off + 256;
 }
@@ -1548,7 +1548,7 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
     if (l == L - 1 && value) {
       // s_b = sum w . (W_{L-1} * adot_{L-2}) = sum (W_{L-1}^T w) . adot_{L-2}
       const long per = (long)n->L[l].cin * n->P;
-      INF_TRY(glue_batched_dot(gb.gad, X_tan, value, B, per, s));
+      INF_TRY(glue_batched_dot(gb.gad, X_tan, value, B, per, gb.bpart, s));
     }
     if (l > 0) {
       const WLayer& prev = n->L[l - 1];

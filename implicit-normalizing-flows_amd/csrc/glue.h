@@ -10,7 +10,8 @@ int glue_normal_logprob(const float* z, float* out, int B, int per, hipStream_t 
 int glue_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, hipStream_t s);
 int glue_poison_lds(hipStream_t s);
 int glue_add(const float* a, const float* b, float* out, long n, hipStream_t s);
-int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, hipStream_t s);
+size_t glue_batched_dot_scratch(int B, long per);
+int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, double* scratch, hipStream_t s);
 int glue_recomp(const float* fx, const float* fz, const float* x, float* out, long n, hipStream_t s);
 int glue_fixed_point_check(const float* x, const float* xp, const float* y, long n, float eps, unsigned int* count,
                            hipStream_t s);

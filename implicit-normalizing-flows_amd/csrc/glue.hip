@@ -186,17 +186,30 @@ int glue_recomp(const float* fx, const float* fz, const float* x, float* out, lo
   return INF_OK;
 }
 
-// out[b] = sum_i a[b][i] * c[b][i]  (fp64, one workgroup per sample)
-__global__ __launch_bounds__(256) void batched_dot_kernel(const float* a, const float* c, float* out, long per) {
+// out[b] = sum_i a[b][i] * c[b][i]: fp64 partials over (chunk, sample), then a fixed-order sum per sample
+constexpr int DOT_CHUNK = 16384;
+__global__ __launch_bounds__(256) void batched_dot_partial_kernel(const float* a, const float* c, double* part,
+                                                                  long per, int nchunk) {
   __shared__ double red[16];
-  const long base = (long)blockIdx.x * per;
+  const int ch = blockIdx.x, b = blockIdx.y;
+  const long base = (long)b * per, lo = (long)ch * DOT_CHUNK, hi = min(per, lo + DOT_CHUNK);
   double acc = 0.0;
-  for (long i = threadIdx.x; i < per; i += blockDim.x) acc += (double)a[base + i] * (double)c[base + i];
+  for (long i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += (double)a[base + i] * (double)c[base + i];
   const double t = block_sum(acc, red);
-  if (threadIdx.x == 0) out[blockIdx.x] = (float)t;
+  if (threadIdx.x == 0) part[(long)b * nchunk + ch] = t;
 }
-int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, hipStream_t s) {
-  hipLaunchKernelGGL(batched_dot_kernel, dim3(B), dim3(256), 0, s, a, c, out, per);
+__global__ void batched_dot_final_kernel(const double* part, int nchunk, int B, float* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double s = 0.0;
+  for (int k = 0; k < nchunk; ++k) s += part[(long)b * nchunk + k];
+  out[b] = (float)s;
+}
+size_t glue_batched_dot_scratch(int B, long per) { return (size_t)B * ((per + DOT_CHUNK - 1) / DOT_CHUNK); }
+int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, double* scratch, hipStream_t s) {
+  const int nchunk = (int)((per + DOT_CHUNK - 1) / DOT_CHUNK);
+  hipLaunchKernelGGL(batched_dot_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, a, c, scratch, per, nchunk);
+  hipLaunchKernelGGL(batched_dot_final_kernel, dim3((B + 63) / 64), dim3(64), 0, s, scratch, nchunk, B, out);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

@@ -99,6 +99,168 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
   }
 }
 
+// Tiled variant for P % 32 == 0 (every conv-net weight gradient): each wave owns TMW x TNW 32x32 MFMA
+// tiles (block tile 64*TMW x 64*TNW, 4 waves as 2 x 2), split boundaries at 32-pixel chunks (a chunk never
+// straddles images, so its image / pixel index is computed once), and the next chunk's operands are
+// loaded into registers while the current chunk's MFMAs run.
+template <int TMW, int TNW>
+__global__ __launch_bounds__(256) void wgrad_tiled_kernel(WgradArgs a) {
+  constexpr int BM = 64 * TMW, BN = 64 * TNW;
+  constexpr int GPT = BM * WG_K / 256, XPT = BN * WG_K / 256;      // elements per thread per chunk
+  __shared__ float Gs[BM][WG_LD];
+  __shared__ float Xs[BN][WG_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+  const long nchunks = (long)a.B * a.P / WG_K;
+  const long c_lo = (nchunks * split) / a.nsplit, c_hi = (nchunks * (split + 1)) / a.nsplit;
+  const float bs = a.x_beta ? softplus_f(*a.x_beta) : 0.f;
+  const int kk9 = a.ks * a.ks, r = a.ks / 2;
+  // fixed (row, pixel-in-chunk) assignment: element j of thread tid is row (tid + 256 j) / 32
+  int grow[GPT], xrow[XPT], gkk[GPT], xkk[XPT], xi[XPT], xdy[XPT], xdx[XPT];
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int e = tid + 256 * j;
+    grow[j] = e / WG_K;
+    gkk[j] = e % WG_K;
+  }
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int e = tid + 256 * j;
+    xrow[j] = e / WG_K;
+    xkk[j] = e % WG_K;
+    const int n = n0 + xrow[j];
+    const int i = n / kk9, t = n - i * kk9;
+    xi[j] = n < a.N ? i : -1;
+    xdy[j] = t / a.ks - r;
+    xdx[j] = t % a.ks - r;
+  }
+  float gv[GPT], xv[XPT];
+  auto load = [&](long c) {
+    const long k0 = c * WG_K;
+    const long b = k0 / a.P;
+    const int p0 = (int)(k0 - b * a.P);
+    const float* Gb = a.G + b * a.g_sample;
+    const float* Xb = a.X + b * a.x_sample;
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+      const int m = m0 + grow[j];
+      gv[j] = m < a.M ? Gb[(long)m * a.P + p0 + gkk[j]] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) {
+      float v = 0.f;
+      if (xi[j] >= 0) {
+        const int p = p0 + xkk[j];
+        const int py = p / a.W, px = p - py * a.W;
+        const int yy = py + xdy[j], xx = px + xdx[j];
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+          v = Xb[(long)xi[j] * a.P + yy * a.W + xx];
+          if (a.x_beta) v = swish_f(v, bs);
+        }
+      }
+      xv[j] = v;
+    }
+  };
+  f32x16 acc[TMW][TNW];
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TNW; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int wm = (wid & 1) * 32 * TMW, wn = (wid >> 1) * 32 * TNW;
+  const int l = lane & 31, h = lane >> 5;
+  if (c_lo < c_hi) load(c_lo);
+  for (long c = c_lo; c < c_hi; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) Gs[grow[j]][gkk[j]] = gv[j];
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) Xs[xrow[j]][xkk[j]] = xv[j];
+    __syncthreads();
+    if (c + 1 < c_hi) load(c + 1);          // in flight under this chunk's MFMAs
+#pragma unroll
+    for (int st = 0; st < WG_K / 2; ++st) {
+      float av[TMW], bv[TNW];
+#pragma unroll
+      for (int i = 0; i < TMW; ++i) av[i] = Gs[wm + 32 * i + l][2 * st + h];
+#pragma unroll
+      for (int j = 0; j < TNW; ++j) bv[j] = Xs[wn + 32 * j + l][2 * st + h];
+#pragma unroll
+      for (int i = 0; i < TMW; ++i)
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* out = a.slab + (long)split * a.M * a.N;
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TNW; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int n = n0 + wn + 32 * j + l;
+        if (m < a.M && n < a.N) out[(long)m * a.N + n] = acc[i][j][q];
+      }
+}
+
+// Small-M variant (M <= 16: the last 3x3 layer, whose cout is the image channel count, and its dsigma):
+// VALU, one output column n per thread with all M accumulators in registers; the split runs over
+// (image, row) ranges and the pixel loop is uniform, so G[m][pixel] are scalar loads and the tap bounds
+// checks are uniform branches.
+constexpr int WGV_MAXM = 16;
+__global__ __launch_bounds__(256) void wgrad_valu_kernel(WgradArgs a) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int split = blockIdx.y;
+  const long rows = (long)a.B * a.H;
+  const long r_lo = (rows * split) / a.nsplit, r_hi = (rows * (split + 1)) / a.nsplit;
+  const float bs = a.x_beta ? softplus_f(*a.x_beta) : 0.f;
+  const int kk9 = a.ks * a.ks, rr = a.ks / 2;
+  const bool valid = n < a.N;
+  const int i = valid ? n / kk9 : 0, t = valid ? n - i * kk9 : 0;
+  const int dy = t / a.ks - rr, dx = t % a.ks - rr;
+  float acc[WGV_MAXM];
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m) acc[m] = 0.f;
+  for (long row = r_lo; row < r_hi; ++row) {
+    const long b = row / a.H;
+    const int y = (int)(row - b * a.H);
+    const int yy = y + dy;
+    const bool yin = valid && yy >= 0 && yy < a.H;
+    const float* xr = a.X + b * a.x_sample + (long)i * a.P + (long)yy * a.W;
+    const float* gr = a.G + b * a.g_sample + (long)y * a.W;
+    // W % 8 == 0 (host check): 8 independent gathers in flight, then 2 uniform float4 G loads per m
+    for (int x0 = 0; x0 < a.W; x0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int xx = x0 + u + dx;
+        v[u] = (yin && xx >= 0 && xx < a.W) ? xr[xx] : 0.f;
+      }
+      if (a.x_beta) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = swish_f(v[u], bs);
+      }
+#pragma unroll
+      for (int m = 0; m < WGV_MAXM; ++m)
+        if (m < a.M) {
+          const float4 g0 = *reinterpret_cast<const float4*>(gr + (long)m * a.P + x0);
+          const float4 g1 = *reinterpret_cast<const float4*>(gr + (long)m * a.P + x0 + 4);
+          acc[m] = fmaf(g0.x, v[0], acc[m]); acc[m] = fmaf(g0.y, v[1], acc[m]);
+          acc[m] = fmaf(g0.z, v[2], acc[m]); acc[m] = fmaf(g0.w, v[3], acc[m]);
+          acc[m] = fmaf(g1.x, v[4], acc[m]); acc[m] = fmaf(g1.y, v[5], acc[m]);
+          acc[m] = fmaf(g1.z, v[6], acc[m]); acc[m] = fmaf(g1.w, v[7], acc[m]);
+        }
+    }
+  }
+  if (!valid) return;
+  float* out = a.slab + (long)split * a.M * a.N;
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m)
+    if (m < a.M) out[(long)m * a.N + n] = acc[m];
+}
+
 // out[i] = sum_s slab[s][i] (fp64, fixed order) (* scale)
 __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float* out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,6 +272,53 @@ __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float*
 
 int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
+  if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0) {
+    const int nb = (a.N + 255) / 256;
+    const long rows = (long)a.B * a.H;
+    int nsplit = (int)std::max<long>(1, std::min<long>(rows, 2048 / std::max(1, nb)));
+    if (nsplit > a.max_split) nsplit = a.max_split;
+    a.nsplit = nsplit;
+    const bool prof = prof_enabled();
+    if (prof) prof_begin_launch(s);
+    hipLaunchKernelGGL(wgrad_valu_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
+    INF_CHECK_LAUNCH();
+    if (prof) {
+      const double K = (double)a.B * a.P;
+      prof_end_launch(s, 899, 2.0 * a.M * a.N * K, 4.0 * K * (a.M + (double)a.N / (a.ks * a.ks)));
+    }
+    const long n = (long)a.M * a.N;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.slab, nsplit, n,
+                       a.out);
+    INF_CHECK_LAUNCH();
+    return INF_OK;
+  }
+  if (a.P % WG_K == 0) {
+    // 128-wide tiles along dims that fill them, 64 otherwise
+    const int tmw = a.M >= 128 ? 2 : 1, tnw = a.N >= 128 ? 2 : 1;
+    const int bm = 64 * tmw, bn = 64 * tnw;
+    const int mt = (a.M + bm - 1) / bm, nt = (a.N + bn - 1) / bn;
+    const long nchunks = (long)a.B * a.P / WG_K;
+    int nsplit = (int)std::max<long>(1, std::min<long>(nchunks / 4, 1024 / std::max(1, mt * nt)));
+    if (nsplit > a.max_split) nsplit = a.max_split;
+    a.nsplit = nsplit;
+    const dim3 grid(mt, nt, nsplit);
+    const bool prof = prof_enabled();
+    if (prof) prof_begin_launch(s);
+    if (tmw == 2 && tnw == 2) hipLaunchKernelGGL((wgrad_tiled_kernel<2, 2>), grid, dim3(256), 0, s, a);
+    else if (tmw == 2) hipLaunchKernelGGL((wgrad_tiled_kernel<2, 1>), grid, dim3(256), 0, s, a);
+    else if (tnw == 2) hipLaunchKernelGGL((wgrad_tiled_kernel<1, 2>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_tiled_kernel<1, 1>), grid, dim3(256), 0, s, a);
+    INF_CHECK_LAUNCH();
+    if (prof) {
+      const double K = (double)a.B * a.P;
+      prof_end_launch(s, 800 + 10 * tmw + tnw, 2.0 * a.M * a.N * K, 4.0 * K * (a.M + (double)a.N / (a.ks * a.ks)));
+    }
+    const long n = (long)a.M * a.N;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.slab, nsplit, n,
+                       a.out);
+    INF_CHECK_LAUNCH();
+    return INF_OK;
+  }
   const int mt = (a.M + WG_T - 1) / WG_T, nt = (a.N + WG_T - 1) / WG_T;
   const long Ktot = (long)a.B * a.P;
   int nsplit = (int)std::max<long>(1, std::min<long>(Ktot / 256, 1024 / std::max(1, mt * nt)));
@@ -197,12 +406,21 @@ __global__ void beta_reduce_kernel(const double* bpart, int n, float* out, int a
 // Lipschitz normalisation (mixed_lipschitz.py:126-131,378-385): W_eff = W / f, f = max(1, sigma / coeff),
 // sigma = u . (W v).  dW = dW_eff / f - [sigma / coeff > 1] <dW_eff, W> / (f^2 coeff) dsigma/dW.
 // dot = <dW_eff, W> (fp64, one block), then the elementwise combine.
-__global__ __launch_bounds__(1024) void sigma_dot_kernel(const float* dWe, const float* W, long n, double* dot) {
+constexpr int SDOT_BLOCKS = 64;
+__global__ __launch_bounds__(256) void sigma_dot_partial_kernel(const float* dWe, const float* W, long n,
+                                                                double* part) {
   __shared__ double red[16];
   double acc = 0.0;
-  for (long i = threadIdx.x; i < n; i += blockDim.x) acc += (double)dWe[i] * (double)W[i];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    acc += (double)dWe[i] * (double)W[i];
   const double t = block_sum(acc, red);
-  if (threadIdx.x == 0) dot[0] = t;
+  if (threadIdx.x == 0) part[1 + blockIdx.x] = t;
+}
+__global__ void sigma_dot_final_kernel(double* dot) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int k = 0; k < SDOT_BLOCKS; ++k) s += dot[1 + k];
+  dot[0] = s;
 }
 __global__ void sigma_chain_kernel(const float* dWe, const float* dsig, const float* factor, float coeff,
                                    const double* dot, float* dW, long n) {
@@ -244,7 +462,8 @@ int launch_beta_reduce(const double* bpart, int n, float* out, int accumulate, h
 }
 int launch_sigma_chain(const float* dWe, const float* W, const float* dsig, const float* factor, float coeff,
                        double* dot, float* dW, long n, hipStream_t s) {
-  hipLaunchKernelGGL(sigma_dot_kernel, dim3(1), dim3(1024), 0, s, dWe, W, n, dot);
+  hipLaunchKernelGGL(sigma_dot_partial_kernel, dim3(SDOT_BLOCKS), dim3(256), 0, s, dWe, W, n, dot);
+  hipLaunchKernelGGL(sigma_dot_final_kernel, dim3(1), dim3(64), 0, s, dot);
   hipLaunchKernelGGL(sigma_chain_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dWe, dsig, factor, coeff,
                      dot, dW, n);
   INF_CHECK_LAUNCH();

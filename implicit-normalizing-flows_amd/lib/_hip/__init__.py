@@ -307,6 +307,10 @@ def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
     if 500 <= tag < 530:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide)
         return 'net313_kernel%s<%s>' % (['', '_h', '_w'][(tag - 500) // 10], ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
+    if tag == 899:
+        return 'wgrad_valu_kernel'
+    if 800 <= tag < 900:     # weight-gradient kernel (grad.hip), 8<TMW><TNW>
+        return 'wgrad_tiled_kernel<%d,%d>' % ((tag - 800) // 10, tag % 10)
     if tag < 1000:
         modes = {0: 'PLAIN', 1: 'EMBED', 2: 'RESID', 3: 'RECOMP', 4: 'VJP'}
         return 'conv_out_kernel<%d> mode %s' % (tag % 10, modes.get((tag - 900) // 10, '?'))
