@@ -42,6 +42,15 @@ METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs 
     'celebahq256': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CelebA-HQ 256 density eval',
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA peak (1024 flop/clk/SIMD x 1024 SIMDs x 2.4 GHz)
+# The fused net kernel's default arithmetic (INF_MFMA_BF16X6, include/inflow.h): every fp32 operand split exactly
+# into three bf16 pieces, six bf16 MFMA products per fp32 product -> fp32-equivalent peak = bf16 peak / 6.
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
+
+
+def mfma_mode():
+    """Arithmetic of the fused kernels, as inf_net_create picks it (INFLOW_MFMA=f32 selects exact fp32 MFMA)."""
+    return 'f32' if os.environ.get('INFLOW_MFMA', '').startswith('f') else 'bf16x6'
 HBM_PEAK_GBS = 8000.0
 
 
@@ -54,7 +63,7 @@ def parse():
     ap.add_argument('--config', default='cifar10', choices=['cifar10', 'cifar10_small', 'celebahq256'])
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
-    ap.add_argument('--cpu-batch', type=int, default=2)
+    ap.add_argument('--cpu-batch', type=int, default=16, help='images in the bounded CPU-baseline sample (~10-15 s)')
     ap.add_argument('--mode', default='eval', choices=['eval', 'train'],
                     help='eval: the density-evaluation hot path (BASELINE metric); train: one training step '
                          '(train-mode forward + loss.backward(), train_img.py:611-638; no optimizer step)')
@@ -164,12 +173,18 @@ def main():
 
     if torch.is_tensor(bpd):
         bpd = float(bpd)
+    mm = mfma_mode()
+    fused_dom = 'net313' in _hip.tag_name(dom['tag'])
+    peak = X6_PEAK_TFLOPS if (mm == 'bf16x6' and fused_dom) else FP32_MFMA_PEAK_TFLOPS
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
         'samples/sec (whole node), %s training step (forward + backward)' % args.config,
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'mfma': ('bf16x6: fp32 operands split exactly into 3 bf16 pieces, 6 products per fp32 product, fp32 '
+                 'accumulation (error at fp32 level, tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)'
+                 if mm == 'bf16x6' else 'f32: v_mfma_f32_32x32x2_f32'),
         'data': 'synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
                 % 'x'.join(map(str, arch['input_size'])),
         'config': {'workload': '%s implicit flow density eval (run_cifar10.sh arch%s), batch %d per GPU'
@@ -178,7 +193,10 @@ def main():
                    'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps},
         'bits_per_dim': round(bpd, 6),
         'roofline': {'bound': 'mfma', 'kernel': _hip.tag_name(dom['tag']), 'achieved': round(achieved, 2),
-                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     'peak': round(peak, 1), 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4),
+                     'peak_basis': ('fp32-equivalent: dense bf16 MFMA peak %.1f / 6 products' % BF16_MFMA_PEAK_TFLOPS
+                                    if peak != FP32_MFMA_PEAK_TFLOPS else 'dense fp32 MFMA peak'),
+                     'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not bf16 MFMA FLOPs',
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
                      'flops_per_launch': dom['flops'] / dom['launches']},
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),

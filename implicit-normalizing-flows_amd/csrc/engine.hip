@@ -91,6 +91,9 @@ struct InfNet {
   bool fused = false;
   int fhid = 0, K1pad = 0, M3 = 0, M3pad = 0;
   float *F1f = nullptr, *F1b = nullptr, *F2f = nullptr, *F2b = nullptr, *F3f = nullptr, *F3b = nullptr;
+  // F1f..F3b split into three bf16 planes each (launch_split3), same order as F1f..F3b
+  uint16_t* Fs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int mfma_mode = INF_MFMA_F32;                 // InfMfmaMode of the fused kernel's phase B
   // f(0) of a conv net (the same image for every sample: zero input, zero padding), cached for the first
   // Broyden residual; computed by a launch of the same batch size (same tile variant -> same bits)
   float* f0 = nullptr;
@@ -217,6 +220,10 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.K1pad = n->K1pad;
   f.A2 = vjp ? n->F2b : n->F2f;
   f.A3 = vjp ? n->F3b : n->F3f;
+  const bool spl = n->mfma_mode == INF_MFMA_BF16X6;
+  f.A1s = spl ? (const void*)n->Fs[vjp ? 1 : 0] : nullptr;
+  f.A2s = spl ? (const void*)n->Fs[vjp ? 3 : 2] : nullptr;
+  f.A3s = spl ? (const void*)n->Fs[vjp ? 5 : 4] : nullptr;
   f.M3 = n->M3;
   f.M3pad = n->M3pad;
   f.b1 = n->L[0].b;
@@ -855,7 +862,11 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       n->M3 = 9 * n->C;
       n->M3pad = round_up(9 * n->C, 32);
       floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
+      // split planes: 3 bf16 (= 1.5 floats) per element of each of the six operands
+      floats += 3 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
       n->rows_max = std::max(n->rows_max, n->M3);
+      const char* mm = getenv("INFLOW_MFMA");             // "f32" / "bf16x6" (default)
+      n->mfma_mode = (mm && mm[0] == 'f') ? INF_MFMA_F32 : INF_MFMA_BF16X6;
     }
   }
   // sigma scratch: one partial per 256 output elements of the largest conv
@@ -886,10 +897,21 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       *bufs[i] = p;
       p += sz[i] + 64;
     }
+    for (int i = 0; i < 6; ++i) {
+      n->Fs[i] = reinterpret_cast<uint16_t*>(p);
+      p += (3 * sz[i] + 1) / 2 + 64;
+    }
   }
   *out = n;
   return INF_OK;
 }
+
+int inf_net_set_mfma(InfNet* n, int mode) {
+  if (!n || (mode != INF_MFMA_F32 && mode != INF_MFMA_BF16X6)) return INF_ERR_INVALID;
+  n->mfma_mode = mode;
+  return INF_OK;
+}
+int inf_net_get_mfma(const InfNet* n) { return n ? n->mfma_mode : -1; }
 
 int inf_net_destroy(InfNet* n) {
   if (!n) return INF_OK;
@@ -920,6 +942,10 @@ int inf_net_refresh(InfNet* n, void* stream) {
     INF_TRY(launch_pack(l1.W, l1.factor, n->F2b, H, H, 1, H, H, PK_TRANSPOSE, s, 1));
     INF_TRY(launch_pack(l2.W, l2.factor, n->F3f, l2.cout, l2.cin, 3, n->M3pad, H, PK_TAPS_FWD, s, 1));
     INF_TRY(launch_pack(l0.W, l0.factor, n->F3b, l0.cout, l0.cin, 3, n->M3pad, H, PK_TAPS_BWD, s, 1));
+    const float* src[6] = {n->F1f, n->F1b, n->F2f, n->F2b, n->F3f, n->F3b};
+    const long cnt[6] = {(long)H * n->K1pad, (long)H * n->K1pad, (long)H * H, (long)H * H, (long)n->M3pad * H,
+                         (long)n->M3pad * H};
+    for (int i = 0; i < 6; ++i) INF_TRY(launch_split3(src[i], n->Fs[i], cnt[i], s));
   }
   return INF_OK;
 }

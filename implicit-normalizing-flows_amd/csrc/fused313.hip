@@ -23,7 +23,13 @@
 // dwordx4 loads per row block (no LDS for A).  B fragments come from LDS: one ds_read2_b32 per
 // MFMA k-step (32 lanes read 32 consecutive floats: conflict-free).
 // 8 waves x (TM*32 rows) cover HID = 256*TM rows; each wave owns 2 x 32 pixel columns.
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <map>
+#include <string>
+
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -45,12 +51,63 @@ __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = v1.w;
 }
 
+// ---- split-bf16 ("x6") contraction: fp32-level products at the bf16 MFMA rate ----------------------
+// x = hi + mid + lo exactly (truncation: hi = top 16 bits, mid = top 16 bits of x - hi, lo = the rest,
+// which has <= 8 significant bits).  x.w ~ hh + hm + mh + hl + lh + mm; the dropped ml, lm, ll terms are
+// <= ~2^-23 |x||w|, the size of fp32's own rounding.  v_mfma_f32_32x32x16_bf16 takes the same k-slots per
+// lane as 8 consecutive v_mfma_f32_32x32x2_f32 steps (lane l: row/column l&31, k = 8 (l>>5) + 0..7), so
+// the fragment-major layouts carry over unchanged: 6 bf16 MFMAs (32 cycles each) replace 8 fp32 ones
+// (64 cycles each).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split3(const float (&x)[8], u32x4& h, u32x4& m, u32x4& l) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned u0 = __float_as_uint(x[2 * j]), u1 = __float_as_uint(x[2 * j + 1]);
+#ifdef INFLOW_SPLIT_PK
+    const f32x2 xv = {x[2 * j], x[2 * j + 1]};
+    const f32x2 hv = {__uint_as_float(u0 & 0xffff0000u), __uint_as_float(u1 & 0xffff0000u)};
+    const f32x2 r = xv - hv;                                  // v_pk_add_f32 (exact)
+    const unsigned v0 = __float_as_uint(r.x), v1 = __float_as_uint(r.y);
+    const f32x2 mv = {__uint_as_float(v0 & 0xffff0000u), __uint_as_float(v1 & 0xffff0000u)};
+    const f32x2 sl = r - mv;                                  // exact, <= 8 significant bits
+    const float s0 = sl.x, s1 = sl.y;
+#else
+    const float r0 = x[2 * j] - __uint_as_float(u0 & 0xffff0000u);       // exact
+    const float r1 = x[2 * j + 1] - __uint_as_float(u1 & 0xffff0000u);
+    const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);             // exact, <= 8 significant bits
+    const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+#endif
+    h[j] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    m[j] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    l[j] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);
+  }
+}
+__device__ __forceinline__ f32x16 mfma_bf16(const u32x4& a, const u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                 0, 0, 0);
+}
+// acc += A.B with A = (a[0], a[1], a[2]) pre-split planes, B = (h, m, l); small terms first
+__device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4& h, const u32x4& m, const u32x4& l,
+                                         f32x16 c) {
+  c = mfma_bf16(a[0], l, c);
+  c = mfma_bf16(a[2], h, c);
+  c = mfma_bf16(a[1], m, c);
+  c = mfma_bf16(a[0], m, c);
+  c = mfma_bf16(a[1], h, c);
+  c = mfma_bf16(a[0], h, c);
+  return c;
+}
+
 // fragment-major offset of (row block rb, k tile kt) for a matrix with nkt K tiles
 __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;
 }
 
-template <int TM, int MODE, int F_BN, int F_LDS_FLOATS, int NW = 8>
+template <int TM, int MODE, int F_BN, int F_LDS_FLOATS, int SPL = 0, int NW = 8>
 __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   constexpr int NT = 64 * NW;                        // threads per workgroup
   constexpr int HID = NW * 32 * TM;
@@ -60,6 +117,11 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   const Net313Args& a = pr.a[sel];
   const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
+#define STAMP(i_)                                                                            \
+  do {                                                                                       \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * 8 + (i_)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  STAMP(0);
   float* t = smem;                                  // [HID][64] activation tile
   int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
   float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
@@ -85,51 +147,67 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   const float* in = a.in + (long)img * a.C * P;
   const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
   double dacc = 0.0;
-  if (a.in_taps) {
+  if (pr.dbg & 8) {
+  } else if (a.in_taps) {
     const float* ytap = a.in_taps + (long)img * a.M3 * P;
     const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
     const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
     const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
-    // 4 halo elements per pass with unconditional (clamped-address) loads: 36 tap loads in flight
-    // per thread instead of one bounds-checked chain per element.
-    constexpr int SU = 4;
-    for (int i0 = tid; i0 < vhz; i0 += NT * SU) {
-      float tv[SU][9], xm[SU], ev[SU];
-      int ok[SU];
-      long ee[SU];
+    // Up to 4 halo elements per pass with unconditional (clamped-address) loads, all issued before any
+    // is used: 44 loads in flight per thread instead of one bounds-checked chain per element.  The pass
+    // width NU is wave-uniform and a compile-time constant per branch (a runtime slot guard lets the
+    // compiler fuse each slot's loads with their use), so a small halo costs one pass of 11 loads.
+    const float* mxp = mx ? mx : ytap;
+    const float* epp = ep ? ep : ytap;
+    auto pass = [&](auto nuc, int i0) {
+      constexpr int NU = decltype(nuc)::value;
+      float tv[NU][9], xm[NU], ev[NU];
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const int i = i0 + u * NT;
         const int ic = i < vhn ? i : 0;
         const int c = ic / (RH * CW), rr = ic - c * RH * CW;
         const int hy = rr / CW, hx = rr - hy * CW;
-        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-        ok[u] = in_img ? ((hy >= 1 && hy <= rows && hx >= 1 && hx <= seg) ? 2 : 1) : 0;
-        const int yq = min(max(yy, 0), a.H - 1), xq = min(max(xx, 0), a.W - 1);
-        ee[u] = (long)c * P + yq * a.W + xq;
+        const int yq = min(max(y0 + hy - 1, 0), a.H - 1), xq = min(max(x0 + hx - 1, 0), a.W - 1);
+        const long ee = (long)c * P + yq * a.W + xq;
         const float* yc = ytap + (long)c * 9 * P;
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
-          const int y2 = yq + tp / 3 - 1, x2 = xq + tp % 3 - 1;
-          const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
-          const float val = yc[(long)tp * P + min(max(y2, 0), a.H - 1) * a.W + min(max(x2, 0), a.W - 1)];
-          tv[u][tp] = vt ? val : 0.f;
+          const int y2 = min(max(yq + tp / 3 - 1, 0), a.H - 1), x2 = min(max(xq + tp % 3 - 1, 0), a.W - 1);
+          tv[u][tp] = yc[(long)tp * P + y2 * a.W + x2];
         }
-        xm[u] = mx ? mx[ee[u]] : 1.f;
-        ev[u] = ep ? ep[ee[u]] : 0.f;
+        xm[u] = mxp[ee];
+        ev[u] = epp[ee];
       }
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const int i = i0 + u * NT;
+        const int ic = i < vhn ? i : 0;
+        const int rr = ic % (RH * CW);
+        const int hy = rr / CW, hx = rr - hy * CW;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+        const int ok = in_img ? ((hy >= 1 && hy <= rows && hx >= 1 && hx <= seg) ? 2 : 1) : 0;
         float v = 0.f;
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) v += tv[u][tp];
+        for (int tp = 0; tp < 9; ++tp) {
+          const int y2 = yy + tp / 3 - 1, x2 = xx + tp % 3 - 1;
+          const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
+          v += vt ? tv[u][tp] : 0.f;
+        }
         if (mx) v = v * swish_d(xm[u], msp);
-        v = ok[u] ? v : 0.f;
-        if (ep && ok[u] == 2) dacc += (double)v * (double)ev[u];
+        v = ok ? v : 0.f;
+        if (ep && ok == 2) dacc += (double)v * (double)ev[u];
         if (i < vhz) vh[i] = v;
       }
+    };
+    constexpr int SU = 4;
+    for (int i0 = tid; i0 < vhz; i0 += NT * SU) {
+      const int nu = min(SU, (vhz - (i0 - tid) + NT - 1) / NT);     // wave-uniform
+      if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
+      else if (nu == 3) pass(std::integral_constant<int, 3>(), i0);
+      else if (nu == 2) pass(std::integral_constant<int, 2>(), i0);
+      else pass(std::integral_constant<int, 1>(), i0);
     }
   } else {
     for (int i = tid; i < vhz; i += NT) {
@@ -212,6 +290,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int b = 0; b < NB; ++b) load_d(a.d2, m, b, dmul[m][b]);
   }
   __syncthreads();
+  STAMP(1);
   if (a.dot_part && tid == 0) {
     double s = 0.0;
 #pragma unroll
@@ -233,7 +312,61 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // Static ping-pong A fragments (a runtime-indexed double buffer would make the compiler wait for
   // the prefetch it just issued); the 8 x NB B values of a K tile are read from LDS in one batch.
   zero_acc();
-  {
+  if constexpr (SPL) {
+    const int nkt = a.K1pad / 16;
+    const u32x4* A1s = reinterpret_cast<const u32x4*>(a.A1s);
+    auto ld3 = [&](int m, int kt, u32x4 (&o)[3]) {
+      const u32x4* q = A1s + ((long)((rbw + m) * nkt + kt) * 3) * 64 + lane;
+      o[0] = q[0];
+      o[1] = q[64];
+      o[2] = q[128];
+    };
+    // B operand (im2col gather from the halo tile) one K tile ahead: its LDS reads and split overlap
+    // this tile's MFMAs
+    auto gath = [&](int kt, float (&x)[NB][8]) {
+      const int* kp = koff + kt * 16 + lh * 8;
+      const int4 k0 = *reinterpret_cast<const int4*>(kp);
+      const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
+      const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x[b][kk] = vh[ko[kk] + pix[b]];
+    };
+    u32x4 bh[NB], bm[NB], bl[NB];
+    {
+      float x0[NB][8];
+      gath(0, x0);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) split3(x0[b], bh[b], bm[b], bl[b]);
+    }
+    auto tileA = [&](int kt, const u32x4 (&af)[TM][3]) {
+      float xn[NB][8];
+      gath(min(kt + 1, nkt - 1), xn);
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], bh[b], bm[b], bl[b], acc[m][b]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+    };
+    u32x4 a0[TM][3], a1[TM][3];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ld3(m, 0, a0[m]);
+    for (int kt = 0; kt < nkt; kt += 2) {
+      const bool has1 = kt + 1 < nkt;
+      if (has1) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ld3(m, kt + 1, a1[m]);
+      }
+      tileA(kt, a0);
+      if (kt + 2 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
+      }
+      if (has1) tileA(kt + 1, a1);
+    }
+  } else {
     const int nkt = a.K1pad / 16;
     auto tileA = [&](int kt, const float (&af)[TM][8]) {
       const int* kp = koff + kt * 16 + lh * 8;
@@ -270,6 +403,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       if (has1) tileA(kt + 1, a1);
     }
   }
+  STAMP(2);
   // epilogue A -> t (LDS); SAVE: d1 -> HBM
   {
     const float sp1 = (MODE != MODE_VJP) ? softplus_f(*a.beta1) : 0.f;
@@ -295,10 +429,48 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       }
   }
   __syncthreads();
+  STAMP(3);
 
   // ---------------------------------------------------------------- phase B: K = HID (from LDS)
   zero_acc();
-  {
+  if constexpr (SPL) {
+    constexpr int nkt = HID / 16;
+    const u32x4* A2s = reinterpret_cast<const u32x4*>(a.A2s);
+    auto ld3 = [&](int m, int kt, u32x4 (&o)[3]) {
+      const u32x4* q = A2s + ((long)((rbw + m) * nkt + kt) * 3) * 64 + lane;
+      o[0] = q[0];
+      o[1] = q[64];
+      o[2] = q[128];
+    };
+    auto tileB = [&](int kt, const u32x4 (&af)[TM][3]) {
+      const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
+      u32x4 bh[NB], bm[NB], bl[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float x[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x[kk] = tb[kk * F_BN + 32 * b];
+        split3(x, bh[b], bm[b], bl[b]);
+      }
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], bh[b], bm[b], bl[b], acc[m][b]);
+    };
+    u32x4 a0[TM][3], a1[TM][3];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ld3(m, 0, a0[m]);
+    for (int kt = 0; kt < nkt; kt += 2) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m) ld3(m, kt + 1, a1[m]);
+      tileB(kt, a0);
+      if (kt + 2 < nkt) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
+      }
+      tileB(kt + 1, a1);
+    }
+  } else {
     constexpr int nkt = HID / 16;
     auto tileB = [&](int kt, const float (&af)[TM][8]) {
       const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
@@ -329,6 +501,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       tileB(kt + 1, a1);
     }
   }
+  STAMP(4);
   if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) {
     const float sp2 = softplus_f(*a.beta2);
 #pragma unroll
@@ -350,7 +523,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) load_d(a.d1, m, b, dmul[m][b]);
+        for (int b = 0; b < NB; ++b) {
+          load_d(a.d1, m, b, dmul[m][b]);
+        }
     }
     const float sp2 = (MODE != MODE_VJP) ? softplus_f(*a.beta2) : 0.f;
 #pragma unroll
@@ -371,6 +546,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
     __syncthreads();
+    STAMP(5);
 
     // -------------------------------------------------------------- phase C: taps, K = HID
     // tasks = (32-row block of the M3pad tap rows) x (32-pixel column); split K when there are
@@ -386,19 +562,126 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     float* Y = a.Y + (long)img * a.M3 * P;
     // rounds of 32 jobs (4 per wave); wide nets (9C > 32*32 tap rows per round) take several rounds.
     // The split-K path only occurs with <= 8 jobs, i.e. in a single round.
-    const int nrounds = (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 4 * NW - 1) / (4 * NW);   // half-LDS: 1 (variant_fits)
+    const int nrounds = (pr.dbg & 4) ? 0 : (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 4 * NW - 1) / (4 * NW);   // half-LDS: 1 (variant_fits)
     for (int round = 0; round < nrounds; ++round) {
     const int jbase = round * 4 * NW;
     f32x16 cacc[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int job = jbase + wid + NW * jj;
+    for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
       for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
+    if constexpr (SPL) {
+      const u32x4* A3s = reinterpret_cast<const u32x4*>(a.A3s);
+      auto ld3 = [&](int rb, int kt, u32x4 (&o)[3]) {
+        const u32x4* q = A3s + ((long)(rb * nkt + kt) * 3) * 64 + lane;
+        o[0] = q[0];
+        o[1] = q[64];
+        o[2] = q[128];
+      };
+      auto bread = [&](int b, int kt, float (&x)[8]) {
+        const float* tc = t + (kt * 16 + lh * 8) * F_BN + b * 32 + li;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x[kk] = tc[kk * F_BN];
+      };
+      auto bsplit = [&](int b, int kt, u32x4& h, u32x4& m, u32x4& l) {
+        float x[8];
+        bread(b, kt, x);
+        split3(x, h, m, l);
+      };
+      if (ksplit > 1 || njobs - jbase <= NW) {
+        // at most one job per wave: one K chain of 6 MFMAs per K tile, so the operand stream is
+        // prefetched 3 K tiles ahead (a 1-ahead ping-pong leaves each step waiting on L2 latency)
+        const int job = jbase + wid;
+        if (job < njobs) {
+          const int task = job / ksplit, ks = job - task * ksplit;
+          const int rb = task / NB, b = task % NB;
+          const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is a multiple of 4
+          // B operand one K tile ahead: its LDS reads and split overlap this tile's MFMA chain
+          u32x4 h, m, l;
+          bsplit(b, k_lo, h, m, l);
+          auto step = [&](int kt, const u32x4 (&af)[3]) {
+            float xn[8];
+            bread(b, min(kt + 1, k_hi - 1), xn);
+            cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
+            split3(xn, h, m, l);
+          };
+          if constexpr (F_LDS_FLOATS != LDS_HALF) {
+            u32x4 r0[3], r1[3], r2[3], r3[3];
+            ld3(rb, k_lo, r0);
+            ld3(rb, k_lo + 1, r1);
+            ld3(rb, k_lo + 2, r2);
+            for (int kt = k_lo; kt < k_hi; kt += 4) {
+              ld3(rb, kt + 3, r3);
+              step(kt, r0);
+              if (kt + 4 < k_hi) ld3(rb, kt + 4, r0);
+              step(kt + 1, r1);
+              if (kt + 5 < k_hi) ld3(rb, kt + 5, r1);
+              step(kt + 2, r2);
+              if (kt + 6 < k_hi) ld3(rb, kt + 6, r2);
+              step(kt + 3, r3);
+            }
+          } else {   // 128-VGPR variant: ping-pong only
+            u32x4 r0[3], r1[3];
+            ld3(rb, k_lo, r0);
+            for (int kt = k_lo; kt < k_hi; kt += 2) {
+              ld3(rb, kt + 1, r1);
+              step(kt, r0);
+              if (kt + 2 < k_hi) ld3(rb, kt + 2, r0);
+              step(kt + 1, r1);
+            }
+          }
+        }
+      } else {
+        // ksplit == 1 and several jobs per wave: a wave's jobs share its pixel column (NW % NB == 0),
+        // so pairs of them advance over K in lockstep on one split B fragment per K tile
+        // (groups of G = 2 jobs; G = 1 in the 128-VGPR variant)
+        constexpr int G = (F_LDS_FLOATS == LDS_HALF) ? 1 : 2;
+        const int b = (jbase + wid) % NB;
+#pragma unroll
+        for (int jp = 0; jp < 4 / G; ++jp) {
+          const int job0 = jbase + wid + NW * (G * jp);
+          if (job0 >= njobs) break;
+          bool vj[G];
+          int rbj[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const int job = job0 + NW * g;
+            vj[g] = job < njobs;
+            rbj[g] = vj[g] ? job / NB : job0 / NB;
+          }
+          u32x4 h, m, l;
+          bsplit(b, 0, h, m, l);
+          auto step = [&](int kt, const u32x4 (&af)[G][3]) {
+            float xn[8];
+            bread(b, min(kt + 1, nkt - 1), xn);
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+              if (vj[g]) cacc[G * jp + g] = mfma_x6(af[g], h, m, l, cacc[G * jp + g]);
+            split3(xn, h, m, l);
+          };
+          auto ldg = [&](int kt, u32x4 (&o)[G][3]) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) ld3(rbj[g], kt, o[g]);
+          };
+          u32x4 p0[G][3], q0[G][3];
+          ldg(0, p0);
+          for (int kt = 0; kt < nkt; kt += 2) {
+            ldg(kt + 1, q0);
+            step(kt, p0);
+            if (kt + 2 < nkt) ldg(kt + 2, p0);
+            step(kt + 1, q0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int job = jbase + wid + NW * jj;
       if (job >= njobs) continue;
       const int task = job / ksplit, ks = job - task * ksplit;
       const int rb = task / NB, b = task % NB;
       const float* tcol = t + lh * 8 * F_BN + b * 32 + li;
+      const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is even
       auto tileC = [&](int kt, const float (&af)[8]) {
         float bv[8];
 #pragma unroll
@@ -407,7 +690,6 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int kk = 0; kk < 8; ++kk)
           cacc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk], bv[kk], cacc[jj], 0, 0, 0);
       };
-      const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is even
       float c0[8], c1[8];
       load_frag8(a.A3 + frag_off(rb, k_lo, nkt, lane), c0);
       for (int kt = k_lo; kt < k_hi; kt += 2) {
@@ -417,6 +699,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         tileC(kt + 1, c1);
       }
     }
+    }
+    if (round == 0) STAMP(6);
     if (ksplit == 1) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
@@ -455,20 +739,28 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }
     }   // rounds
   }
+  STAMP(7);
+#undef STAMP
 }
 
-template <int TM, int MODE>
+template <int TM, int MODE, int SPL>
 __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
-  net313_body<TM, MODE, 64, LDS_FULL>(pr);
+  net313_body<TM, MODE, 64, LDS_FULL, SPL>(pr);
 }
 // two workgroups (16 waves) per CU: at most 128 VGPRs
-template <int TM, int MODE>
+template <int TM, int MODE, int SPL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void net313_kernel_h(Net313Pair pr) {
-  net313_body<TM, MODE, 32, LDS_HALF>(pr);
+  net313_body<TM, MODE, 32, LDS_HALF, SPL>(pr);
 }
-template <int TM, int MODE>
+// one wave per SIMD (4 waves x 4 row blocks): the whole register file per wave, so one wave's own
+// instruction stream overlaps its operand split with its MFMAs
+template <int TM, int MODE, int SPL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void net313_kernel_q(Net313Pair pr) {
+  net313_body<2 * TM, MODE, 64, LDS_FULL, SPL, 4>(pr);
+}
+template <int TM, int MODE, int SPL>
 __global__ __launch_bounds__(512) void net313_kernel_w(Net313Pair pr) {
-  net313_body<TM, MODE, 32, LDS_FULL>(pr);
+  net313_body<TM, MODE, 32, LDS_FULL, SPL>(pr);
 }
 enum { V64 = 0, VHALF = 1, VWIDE = 2 };
 
@@ -494,6 +786,49 @@ int net313_supported(int hid, int C, int H, int W) {
 
 // Launch one or two nets (same shape) as one grid.  The 64-pixel tile is used unless the grid would
 // leave CUs idle (fewer than 256 workgroups), then 32-pixel tiles.
+// ---- INFLOW_FUSED_TIMING (development): per-phase s_memtime deltas of wave 0, averaged per kernel
+struct TimingAcc {
+  double sum[7] = {0, 0, 0, 0, 0, 0, 0};
+  long n = 0;
+};
+static std::map<std::string, TimingAcc>& timing_map() {
+  static auto* m = new std::map<std::string, TimingAcc>();   // never destroyed: read by the atexit report
+  return *m;
+}
+static void timing_report() {
+  static const char* names[7] = {"stage", "phaseA", "epiA", "phaseB", "epiB", "phaseC", "store"};
+  for (auto& kv : timing_map()) {
+    fprintf(stderr, "[timing] %-28s n=%6ld", kv.first.c_str(), kv.second.n);
+    for (int i = 0; i < 7; ++i) fprintf(stderr, " %s %.0f", names[i], kv.second.sum[i] / kv.second.n);
+    fprintf(stderr, "\n");
+  }
+}
+static unsigned long long* g_tbuf = nullptr;
+static long g_tbuf_n = 0;
+static unsigned long long* timing_buf(long nwg) {
+  if (nwg > g_tbuf_n) {
+    if (g_tbuf) (void)hipFree(g_tbuf);
+    if (hipMallocManaged(&g_tbuf, nwg * 8 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    g_tbuf_n = nwg;
+    static bool reg = false;
+    if (!reg) { atexit(timing_report); reg = true; }
+  }
+  return g_tbuf;
+}
+static void timing_collect(const char* key, long nwg, hipStream_t s) {
+  if (!g_tbuf) return;
+  (void)hipStreamSynchronize(s);
+  TimingAcc& acc = timing_map()[key];
+  for (long w = 0; w < nwg; ++w) {
+    const unsigned long long* t = g_tbuf + w * 8;
+    bool ok = true;
+    for (int i = 1; i < 8; ++i) ok = ok && t[i] >= t[i - 1];
+    if (!ok) continue;   // e.g. SAVE mode: no phase C stamps
+    for (int i = 0; i < 7; ++i) acc.sum[i] += (double)(t[i + 1] - t[i]);
+    acc.n += 1;
+  }
+}
+
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets) {
   if (layout_nets <= 0) layout_nets = nnets;
   const Net313Args& a0 = args[0];
@@ -527,14 +862,38 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     return v < 1 ? 1 : v;
   }();
   pr.max_ksplit = max_ksplit;
+  static const int dbg = [] {
+    const char* e = getenv("INFLOW_FUSED_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  pr.dbg = dbg;
+  static const bool timing = getenv("INFLOW_FUSED_TIMING") != nullptr;
+  pr.tbuf = nullptr;
+  if (timing) pr.tbuf = timing_buf(pr.nb0 * nnets);
   const unsigned nb = (unsigned)(pr.nb0 * nnets);
+  static const int split_h = [] {
+    const char* e = getenv("INFLOW_SPLIT_H");             // tuning knob: split-bf16 in the 32-px 2-WG/CU variant
+    return e ? atoi(e) : 1;
+  }();
+  const bool split = pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr && (var != VHALF || split_h);
+  static const int quad_env = [] {
+    const char* e = getenv("INFLOW_FUSED_NW");            // tuning knob: 4 = one wave per SIMD (64-px tiles)
+    return e ? atoi(e) : 8;
+  }();
+  const bool quad = quad_env == 4;
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define L313(TM_, MODE_, BN_)                                                                     \
-  do {                                                                                            \
-    if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);   \
-    else if (var == VHALF) hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr); \
-    else hipLaunchKernelGGL((net313_kernel_w<TM_, MODE_>), dim3(nb), dim3(512), 0, s, pr);           \
+#define L313S(TM_, MODE_, SPL_)                                                                         \
+  do {                                                                                                  \
+    if (var == V64 && quad) hipLaunchKernelGGL((net313_kernel_q<TM_, MODE_, SPL_>), dim3(nb), dim3(256), 0, s, pr); \
+    else if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
+    else if (var == VHALF) hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
+    else hipLaunchKernelGGL((net313_kernel_w<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr);           \
+  } while (0)
+#define L313(TM_, MODE_, BN_)            \
+  do {                                   \
+    if (split) L313S(TM_, MODE_, 1);     \
+    else L313S(TM_, MODE_, 0);           \
   } while (0)
 #define L313M(TM_, BN_)                                \
   do {                                                 \
@@ -547,7 +906,13 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   else L313M(1, bn);
 #undef L313M
 #undef L313
+#undef L313S
   INF_CHECK_LAUNCH();
+  if (pr.tbuf) {
+    char key[64];
+    snprintf(key, sizeof(key), "var%d mode%d split%d C%d", var, mode, (int)split, a0.C);
+    timing_collect(key, (long)nb, s);
+  }
   if (prof) {
     const double npx = (double)nnets * a0.B * P;
     const double fA = 2.0 * hid * 9.0 * a0.C, fB = 2.0 * hid * hid;

@@ -102,6 +102,9 @@ enum PackMode { PK_ROWMAJOR = 0, PK_TRANSPOSE = 1, PK_IM2COL_FWD = 2, PK_IM2COL_
 // frag = 1 writes the fragment-major layout of fused313.hip (Mpad multiple of 32, Kpad of 16).
 int launch_pack(const float* W, const float* factor, float* dst, int cout, int cin, int ks, int Mpad, int Kpad,
                 int mode, hipStream_t s, int frag = 0);
+// Split a fragment-major fp32 operand (n = Mpad * Kpad floats) into three bf16 planes per 512-float
+// fragment tile: dst[(tile * 3 + plane) * 512 + w] (fused313.hip split phase B).
+int launch_split3(const float* src, uint16_t* dst, long n, hipStream_t s);
 
 // exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
@@ -128,6 +131,12 @@ struct Net313Args {
   int K1pad;
   const float* A2;        // phase B operand, fragment-major (HID x HID)
   const float* A3;        // phase C operand, fragment-major (M3pad x HID)
+  // A1s / A2s / A3s: the same operands split into three bf16 planes (hi, mid, lo; exact: hi + mid + lo
+  // equals the fp32 value), fragment-major per (row block, K tile, plane); non-null selects the
+  // split-bf16 ("x6") MFMA path of fused313.hip for all three phases
+  const void* A1s;
+  const void* A2s;
+  const void* A3s;
   int M3, M3pad;          // 9C taps rows
   const float* b1;
   const float* beta1;
@@ -150,6 +159,9 @@ struct Net313Pair {
   Net313Args a[2];
   int nb0;                // workgroups of net 0; blocks >= nb0 run net 1
   int max_ksplit;         // cap on phase C's K split (debug knob, INFLOW_FUSED_KSPLIT)
+  unsigned long long* tbuf;   // INFLOW_FUSED_TIMING: per-workgroup s_memtime stamps at phase boundaries
+  int dbg;                // timing-attribution knob (INFLOW_FUSED_DBG, wrong results when set): 1 skip the
+                          // d1 load, 2 skip the d2 load, 4 skip phase C, 8 skip the input staging
 };
 int net313_supported(int hid, int C, int H, int W);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);

@@ -575,6 +575,28 @@ int launch_pack(const float* W, const float* factor, float* dst, int cout, int c
   return INF_OK;
 }
 
+// Exact three-way bf16 split by truncation: hi = top 16 bits of x, r = x - hi (exact), mid = top 16
+// bits of r, lo = r - mid (at most 8 significant bits, so exact in bf16).  hi + mid + lo == x for every
+// finite x whose pieces stay in the normal range.
+__global__ void split3_kernel(const float* src, uint16_t* dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = src[i];
+  const unsigned u = __float_as_uint(x);
+  const float r = x - __uint_as_float(u & 0xffff0000u);
+  const unsigned v = __float_as_uint(r);
+  const float l = r - __uint_as_float(v & 0xffff0000u);
+  const long tile = i >> 9, w = i & 511;
+  dst[(tile * 3 + 0) * 512 + w] = (uint16_t)(u >> 16);
+  dst[(tile * 3 + 1) * 512 + w] = (uint16_t)(v >> 16);
+  dst[(tile * 3 + 2) * 512 + w] = (uint16_t)(__float_as_uint(l) >> 16);
+}
+int launch_split3(const float* src, uint16_t* dst, long n, hipStream_t s) {
+  hipLaunchKernelGGL(split3_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // exact log|det(I + T)| per sample (torch.logdet via LU, implicit_block.py:253-258).  T is stored
 // feature-major as tangents: T[i][j] of sample b at tang[i * ld + (j + 1) * stride_j + b],

@@ -14,6 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libinflow.so')
+LIB_PATH = os.environ.get('INFLOW_LIB', LIB_PATH)   # development knob: an alternative build
 
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
@@ -73,6 +74,8 @@ _SIGS = {
     'inf_net_create': (ctypes.c_int, [ctypes.POINTER(NetDesc), ctypes.POINTER(_P)]),
     'inf_net_destroy': (ctypes.c_int, [_P]),
     'inf_net_refresh': (ctypes.c_int, [_P, _P]),
+    'inf_net_set_mfma': (ctypes.c_int, [_P, ctypes.c_int]),
+    'inf_net_get_mfma': (ctypes.c_int, [_P]),
     'inf_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int]),
     'inf_net_forward': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_net_vjp': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),

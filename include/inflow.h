@@ -82,6 +82,16 @@ int inf_net_destroy(InfNet* net);
  * sigma = u.(W v) on device, W_eff = W / max(1, sigma/coeff), repacked for the MFMA kernels.
  * Call after any parameter change (the Python side tracks tensor versions). */
 int inf_net_refresh(InfNet* net, void* stream);
+/* Arithmetic of the fused 3-1-3 conv kernel's HID x HID contraction (the 1x1 conv, fused313.hip phase B).
+ *   INF_MFMA_F32    v_mfma_f32_32x32x2_f32: exact fp32 products, k-ordered fp32 accumulation.
+ *   INF_MFMA_BF16X6 both operands split exactly into three bf16 pieces (x = hi + mid + lo, truncation),
+ *                   the six products down to 2^-16 relative on v_mfma_f32_32x32x16_bf16, fp32 accumulation:
+ *                   dropped terms <= 2^-23 relative, i.e. fp32-level error at 16x the per-clock MFMA rate.
+ * Default: INFLOW_MFMA=f32 in the environment at inf_net_create selects F32, otherwise BF16X6.
+ * No effect on nets outside the fused path. */
+typedef enum InfMfmaMode { INF_MFMA_F32 = 0, INF_MFMA_BF16X6 = 1 } InfMfmaMode;
+int inf_net_set_mfma(InfNet* net, int mode);
+int inf_net_get_mfma(const InfNet* net);
 /* Workspace for any call below on a net of this shape at this batch size. */
 size_t inf_workspace_bytes(const InfNet* net, int batch, int threshold);
 /* y = nnet(x). */

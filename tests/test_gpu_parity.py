@@ -234,13 +234,15 @@ def test_device_rademacher():
     assert abs(p.mean().item()) < 0.01
 
 
+@pytest.mark.parametrize('mfma', [0, 1])
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3, 5])
-def test_fused_313_matches_generic_path(block, B, monkeypatch):
+def test_fused_313_matches_generic_path(block, B, mfma, monkeypatch):
     """The fused 3-1-3 kernel (fused313.hip) and the generic GEMM chain agree on forward, VJP
     and the log-det series of the full-size CIFAR nets.  Before every call the workspace and the
     LDS of every CU are filled with NaN, so a read of memory the kernels never wrote shows up as
-    NaN deterministically (B=2 takes the 32-pixel split-K tiles, B=16 the 64-pixel tiles)."""
+    NaN deterministically (B=2 takes the 32-pixel split-K tiles, B=16 the 64-pixel tiles).  mfma selects the
+    fused kernel's arithmetic: 0 exact fp32 MFMA, 1 the split-bf16 ("x6") MFMA path."""
     arch = syn.CIFAR10
     outs = {}
     for mode in ('fused', 'generic'):
@@ -253,6 +255,7 @@ def test_fused_313_matches_generic_path(block, B, monkeypatch):
         v = torch.randn(B, *shape).to(DEV)
         net = _hip.native_net(blk.nnet_z, x.shape[1:], x.device)
         assert net.handle
+        _hip.check(net.lib.inf_net_set_mfma(net.handle, mfma), 'set_mfma')
         stream = _hip.stream_of(x)
         net.refresh_if_needed(stream)
         ws = _hip.workspace(x.device, net.ws_bytes(B))
@@ -281,6 +284,47 @@ def test_fused_313_matches_generic_path(block, B, monkeypatch):
         assert torch.isfinite(a).all()
     for a, b in zip(outs['fused'], outs['generic']):
         _close(a, b, rel=1e-5)
+
+
+@pytest.mark.parametrize('block', [0, 1, 2, 4])
+def test_split_bf16_error_at_fp32_level(block):
+    """INF_MFMA_BF16X6 (exact three-way bf16 split, six products per fp32 product) against INF_MFMA_F32 on the
+    full-size CIFAR nets: both forward and VJP measured against an fp64 CPU evaluation of the same net.
+    Tolerance: the split path's max error (relative to max|ref|) <= 1.5x the fp32 MFMA path's + 1e-7,
+    and both <= 2e-6 (fp32 roundoff level)."""
+    arch = syn.CIFAR10
+    B = 4
+    m, sd = _model(arch, B)
+    blk = imblocks(m)[block]
+    prefix, info = _first_block_net(arch, sd, block=block)
+    torch.manual_seed(10 + block)
+    x = torch.randn(B, *info['shape']) * 0.7
+    v = torch.randn(B, *info['shape'])
+    sd64 = {k: (t.double() if t.is_floating_point() else t) for k, t in sd.items()}
+    ref = orc.make_net(sd64, prefix + '.nnet_x', info['net'], arch['coeff'])
+    xr = x.double().requires_grad_(True)
+    y_ref = ref(xr)
+    g_ref = torch.autograd.grad(y_ref, xr, v.double())[0]
+    xd, vd = x.to(DEV), v.to(DEV)
+    net = _hip.native_net(blk.nnet_x, xd.shape[1:], xd.device)
+    stream = _hip.stream_of(xd)
+    net.refresh_if_needed(stream)
+    ws = _hip.workspace(xd.device, net.ws_bytes(B))
+    err = {}
+    for mode in (0, 1):
+        _hip.check(net.lib.inf_net_set_mfma(net.handle, mode), 'set_mfma')
+        assert net.lib.inf_net_get_mfma(net.handle) == mode
+        y = torch.empty_like(xd)
+        g = torch.empty_like(xd)
+        _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(xd), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
+                                           stream), 'fwd')
+        _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(xd), _hip.ptr(vd), _hip.ptr(g), B, _hip.ptr(ws),
+                                       ws.numel(), stream), 'vjp')
+        torch.cuda.synchronize()
+        err[mode] = [((a.double().cpu() - r).abs().max() / r.abs().max()).item() for a, r in ((y, y_ref), (g, g_ref))]
+    for e32, e6 in zip(err[0], err[1]):
+        assert e32 <= 2e-6 and e6 <= 2e-6, err
+        assert e6 <= 1.5 * e32 + 1e-7, err
 
 
 @pytest.mark.parametrize('kind', ['conv3', 'conv1', 'linear', 'conv3_fixed', 'conv3_cifar'])
@@ -318,7 +362,8 @@ def test_power_iteration_matches_host(kind):
 
 
 @pytest.mark.parametrize('C,H', [(48, 64), (192, 32)])
-def test_fused_wide_variant_matches_generic(C, H, monkeypatch):
+@pytest.mark.parametrize('mfma', [0, 1])
+def test_fused_wide_variant_matches_generic(C, H, mfma, monkeypatch):
     """CelebA-HQ 256 scales (9C tap rows up to 1728, 64x64 / 32x32): the 32-pixel full-LDS variant
     (net313_kernel_w, several phase-C rounds) against the generic GEMM chain, workspace and LDS
     poisoned with NaN before every call."""
@@ -339,6 +384,7 @@ def test_fused_wide_variant_matches_generic(C, H, monkeypatch):
         monkeypatch.setenv('INFLOW_NO_FUSED', '1' if mode == 'generic' else '0')
         net = _hip.NativeNet(_hip.net_entries(seq), (C, H, H), x.device)   # fresh: reads INFLOW_NO_FUSED
         assert net.handle
+        _hip.check(net.lib.inf_net_set_mfma(net.handle, mfma), 'set_mfma')
         stream = _hip.stream_of(x)
         net.refresh_if_needed(stream)
         ws = torch.empty(net.ws_bytes(B), dtype=torch.uint8, device=DEV)

@@ -35,7 +35,7 @@ def main():
         hbm = 2 * fetch + write
         rows.append({'kernel': k[0], 'grid_threads': k[1], 'dispatches': len(f[k]), 'fetch_size_bytes': fetch,
                      'write_size_bytes': write, 'hbm_bytes_corrected': hbm})
-        if 'net313_kernel<2, 2>' in k[0]:        # tag 502 (64-pixel tiles); the _h variant is tag 512
+        if k[0].startswith('void inf::net313_kernel<2, 2'):   # tag 502 (64-pixel tiles, any MFMA mode); _h is tag 512
             vjp += [hbm] * len(f[k])
     res = {'tag': 502, 'kernel': 'net313_kernel<VJP>', 'batch': a.batch,
            'hbm_bytes_per_launch': sum(vjp) / len(vjp) if vjp else None,
