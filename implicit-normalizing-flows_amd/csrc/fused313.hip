@@ -141,6 +141,22 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // after the halo must cover every pixel offset of the tile: rows * CW floats.
   const int vhz = vhn + rows * CW;
 
+  // split path: phase A's first operand tile is requested before the staging loads (it is an L2 hit and
+  // retires long before the staging data, so it costs the staging nothing and phase A starts without a wait)
+  const int rbw0 = wid * TM;
+  u32x4 pa0[TM][3];
+  constexpr bool PRE_A = SPL && F_LDS_FLOATS != LDS_HALF;   // (not in the 128-VGPR variant)
+  if constexpr (PRE_A) {
+    const u32x4* A1s = reinterpret_cast<const u32x4*>(a.A1s);
+    const int nkt1 = a.K1pad / 16;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      const u32x4* q = A1s + ((long)((rbw0 + m) * nkt1) * 3) * 64 + lane;
+      pa0[m][0] = q[0];
+      pa0[m][1] = q[64];
+      pa0[m][2] = q[128];
+    }
+  }
   // ---- stage the input halo tile (zero padded; forward applies the preact swish) ----
   // Series chaining: the input is the previous VJP's packed taps; the tap sum, the preact swish'
   // multiplier and that term's trace partial (conv_out's OM_VJP work) happen here instead.
@@ -333,8 +349,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) x[b][kk] = vh[ko[kk] + pix[b]];
     };
+    // (the 128-VGPR variant gathers and splits in place)
     u32x4 bh[NB], bm[NB], bl[NB];
-    {
+    if constexpr (PRE_A) {
       float x0[NB][8];
       gath(0, x0);
 #pragma unroll
@@ -342,17 +359,32 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }
     auto tileA = [&](int kt, const u32x4 (&af)[TM][3]) {
       float xn[NB][8];
-      gath(min(kt + 1, nkt - 1), xn);
+      if constexpr (PRE_A) {
+        gath(min(kt + 1, nkt - 1), xn);
+      } else {
+        gath(kt, xn);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+      }
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], bh[b], bm[b], bl[b], acc[m][b]);
+      if constexpr (PRE_A) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+        for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+      }
     };
     u32x4 a0[TM][3], a1[TM][3];
 #pragma unroll
-    for (int m = 0; m < TM; ++m) ld3(m, 0, a0[m]);
+    for (int m = 0; m < TM; ++m) {
+      if constexpr (PRE_A) {
+#pragma unroll
+        for (int p3 = 0; p3 < 3; ++p3) a0[m][p3] = pa0[m][p3];
+      } else {
+        ld3(m, 0, a0[m]);
+      }
+    }
     for (int kt = 0; kt < nkt; kt += 2) {
       const bool has1 = kt + 1 < nkt;
       if (has1) {
@@ -598,12 +630,17 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is a multiple of 4
           // B operand one K tile ahead: its LDS reads and split overlap this tile's MFMA chain
           u32x4 h, m, l;
-          bsplit(b, k_lo, h, m, l);
+          if constexpr (PRE_A) bsplit(b, k_lo, h, m, l);
           auto step = [&](int kt, const u32x4 (&af)[3]) {
-            float xn[8];
-            bread(b, min(kt + 1, k_hi - 1), xn);
-            cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
-            split3(xn, h, m, l);
+            if constexpr (PRE_A) {
+              float xn[8];
+              bread(b, min(kt + 1, k_hi - 1), xn);
+              cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
+              split3(xn, h, m, l);
+            } else {
+              bsplit(b, kt, h, m, l);
+              cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
+            }
           };
           if constexpr (F_LDS_FLOATS != LDS_HALF) {
             u32x4 r0[3], r1[3], r2[3], r3[3];
@@ -650,14 +687,15 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             rbj[g] = vj[g] ? job / NB : job0 / NB;
           }
           u32x4 h, m, l;
-          bsplit(b, 0, h, m, l);
+          if constexpr (PRE_A) bsplit(b, 0, h, m, l);
           auto step = [&](int kt, const u32x4 (&af)[G][3]) {
             float xn[8];
-            bread(b, min(kt + 1, nkt - 1), xn);
+            if constexpr (PRE_A) bread(b, min(kt + 1, nkt - 1), xn);
+            else bsplit(b, kt, h, m, l);
 #pragma unroll
             for (int g = 0; g < G; ++g)
               if (vj[g]) cacc[G * jp + g] = mfma_x6(af[g], h, m, l, cacc[G * jp + g]);
-            split3(xn, h, m, l);
+            if constexpr (PRE_A) split3(xn, h, m, l);
           };
           auto ldg = [&](int kt, u32x4 (&o)[G][3]) {
 #pragma unroll
@@ -724,17 +762,16 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int r = 0; r < 16; ++r) part[(job * 16 + r) * 64 + lane] = cacc[jj][r];
       }
       __syncthreads();
-      // one wave per task sums its ksplit partials
-      for (int task = wid; task < ntask; task += NW) {
+      // every thread sums the ksplit partials of ntask*1024/NT outputs (consecutive threads: consecutive
+      // lanes of one accumulator register, so the LDS reads are conflict-free and the stores coalesced)
+      for (int i = tid; i < ntask * 1024; i += NT) {
+        const int task = i >> 10, rem = i & 1023, r = rem >> 6, ln = rem & 63;
+        float sum = 0.f;
+        for (int ks = 0; ks < ksplit; ++ks) sum += part[((task * ksplit + ks) * 16 + r) * 64 + ln];
         const int rb = task / NB, b = task % NB;
-        const int gcol = gp_rt(b);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float s = 0.f;
-          for (int ks = 0; ks < ksplit; ++ks) s += part[((task * ksplit + ks) * 16 + r) * 64 + lane];
-          const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.M3) Y[(long)row * P + gcol] = s;
-        }
+        const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+        const int n = b * 32 + (ln & 31), py = n / seg;
+        if (row < a.M3) Y[(long)row * P + (y0 + py) * a.W + x0 + (n - py * seg)] = sum;
       }
     }
     }   // rounds
