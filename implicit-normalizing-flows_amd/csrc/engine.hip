@@ -435,7 +435,20 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   memset(&stats, 0, sizeof(stats));
   stats.eps = eps;
 
-  float *x = bf.xa, *xn = bf.xb, *gx = bf.ga, *gn = bf.gb;
+  // Iterates rotate through three buffers {xa, xb, lowest} and f(z) through two {fcur, flow}: the lowest
+  // iterate (and its f) is tracked by pointer instead of copied every time it improves (broyden.py:159-162);
+  // the Bufs pointers are permuted at the end so that bf.lowest / bf.flow name the result.
+  float* xpool[3] = {bf.xa, bf.xb, bf.lowest};
+  float* fpool[2] = {bf.fcur, bf.flow};
+  float *x = xpool[0], *xn = xpool[1], *gx = bf.ga, *gn = bf.gb;
+  float *low = x, *flow = fpool[1];
+  auto free_x = [&]() {
+    for (float* p : xpool)
+      if (p != x && p != low) return p;
+    return xpool[0];
+  };
+  auto next_f = [&]() { bf.fcur = (flow == fpool[0]) ? fpool[1] : fpool[0]; };
+  next_f();
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
   INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
@@ -445,8 +458,12 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   lowest_ss = ss;
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
-  INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
-  if (keep_f) INF_HIP(hipMemcpyAsync(bf.flow, bf.fcur, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  low = x;
+  if (keep_f) {
+    flow = bf.fcur;
+    next_f();
+  }
+  xn = free_x();
   // update = -gx; x_est = x0 + update
   INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
   INF_TRY(launch_axpy_step(x, bf.upd, xn, bf.dx, (long)E, s));
@@ -458,8 +475,11 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     obj = sqrt(total(ss));
     trace.push_back(obj);
     if (obj < lowest) {                                               // :159-162
-      INF_HIP(hipMemcpyAsync(bf.lowest, x, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
-      if (keep_f) INF_HIP(hipMemcpyAsync(bf.flow, bf.fcur, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+      low = x;
+      if (keep_f) {
+        flow = bf.fcur;
+        next_f();
+      }
       lowest = obj;
       lowest_step = nstep;
       lowest_ss = ss;
@@ -498,7 +518,21 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     ba.part = bf.bpart;
     ba.m = (nstep - 1) % T;
     ba.ncols = std::min(nstep, T);
+    xn = free_x();
+    ba.xnew = xn;
     INF_TRY(launch_broyden_update(ba, s));
+  }
+  // name the result: bf.lowest = the lowest iterate, bf.flow = its f; the other buffers become scratch
+  {
+    float* rest[2];
+    int k = 0;
+    for (float* p : xpool)
+      if (p != low && k < 2) rest[k++] = p;
+    bf.lowest = low;
+    bf.xa = rest[0];
+    bf.xb = rest[1];
+    bf.flow = flow;
+    bf.fcur = (flow == fpool[0]) ? fpool[1] : fpool[0];
   }
   stats.nstep = nstep;
   stats.lowest_step = lowest_step;
