@@ -383,7 +383,8 @@ class imBlock(nn.Module):
         n_ps, coeff_fn, ns = plan
         probes = (_probes(x.shape, x.device), _probes(x.shape, x.device))
         co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
-        ws = _hip.workspace(x.device, nx.ws_bytes(B, T) + nz.ws_bytes(B, 1))
+        # the third region lets the engine run the x-branch series beside the root solve (inflow.h)
+        ws = _hip.workspace(x.device, nx.ws_bytes(B, T) + nz.ws_bytes(B, 1) + nx.ws_bytes(B, 1))
         z = torch.empty_like(x)
         out = torch.empty(2, B, device=x.device)
         st = _hip.BroydenStats()

@@ -136,7 +136,9 @@ int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_
  * eps_x / eps_z and coeff[k-1] = (-1)^(k+1)/k coeff_fn(k); logdet_x[b], logdet_z[b] receive the two
  * series (the block's log-det is their difference).  The x_embed pass also saves f_x's derivatives, so
  * only the z-net needs its own.  INF_ERR_UNSUPPORTED when a net is not fused (use the separate calls).
- * ws >= inf_workspace_bytes(net_x, batch, threshold) + inf_workspace_bytes(net_z, batch, 1). */
+ * ws >= inf_workspace_bytes(net_x, batch, threshold) + inf_workspace_bytes(net_z, batch, 1).  With a further
+ * inf_workspace_bytes(net_x, batch, 1) the x-branch series runs on an internal side stream concurrently with
+ * the root solve and the z-branch series (joined into `stream` before return) when INFLOW_EVAL_OVERLAP=1 (off by default). */
 int inf_imblock_eval(InfNet* net_x, InfNet* net_z, const float* x, float* z, const float* eps_x, const float* eps_z,
                      const float* coeff, int n_terms, float* logdet_x, float* logdet_z, int batch, int threshold,
                      double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
