@@ -82,7 +82,7 @@ int inf_net_destroy(InfNet* net);
  * sigma = u.(W v) on device, W_eff = W / max(1, sigma/coeff), repacked for the MFMA kernels.
  * Call after any parameter change (the Python side tracks tensor versions). */
 int inf_net_refresh(InfNet* net, void* stream);
-/* Arithmetic of the fused 3-1-3 conv kernel's HID x HID contraction (the 1x1 conv, fused313.hip phase B).
+/* Arithmetic of the fused 3-1-3 conv kernel's three contractions (fused313.hip phases A, B, C).
  *   INF_MFMA_F32    v_mfma_f32_32x32x2_f32: exact fp32 products, k-ordered fp32 accumulation.
  *   INF_MFMA_BF16X6 both operands split exactly into three bf16 pieces (x = hi + mid + lo, truncation),
  *                   the six products down to 2^-16 relative on v_mfma_f32_32x32x16_bf16, fp32 accumulation:

@@ -361,17 +361,17 @@ def test_power_iteration_matches_host(kind):
     np.testing.assert_allclose(w_dev.cpu().numpy(), w_host.detach().numpy(), rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize('C,H', [(48, 64), (192, 32)])
+@pytest.mark.parametrize('C,H,hid,B', [(48, 64, 512, 2), (192, 32, 512, 2), (3, 32, 256, 8), (12, 16, 256, 2)])
 @pytest.mark.parametrize('mfma', [0, 1])
-def test_fused_wide_variant_matches_generic(C, H, mfma, monkeypatch):
+def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
     """CelebA-HQ 256 scales (9C tap rows up to 1728, 64x64 / 32x32): the 32-pixel full-LDS variant
     (net313_kernel_w, several phase-C rounds) against the generic GEMM chain, workspace and LDS
-    poisoned with NaN before every call."""
+    poisoned with NaN before every call.  hid = 256 nets take the one-row-block-per-wave instantiation
+    (64-pixel tiles at B=8, 32-pixel tiles at B=2)."""
     from lib.layers.base import InducedNormConv2d, Swish
     torch.manual_seed(2)
-    B = 2
     conv = lambda a, b, k: InducedNormConv2d(a, b, k, 1, k // 2, coeff=0.9, atol=1e-3, rtol=1e-3)
-    seq = torch.nn.Sequential(Swish(), conv(C, 512, 3), Swish(), conv(512, 512, 1), Swish(), conv(512, C, 3)).to(DEV)
+    seq = torch.nn.Sequential(Swish(), conv(C, hid, 3), Swish(), conv(hid, hid, 1), Swish(), conv(hid, C, 3)).to(DEV)
     with torch.no_grad():
         seq(torch.zeros(1, C, H, H, device=DEV))             # lazy u/v (engine power iteration)
         for m in seq:
