@@ -115,8 +115,7 @@ def main():
     torch.manual_seed(0)
 
     if args.mode == 'train':
-        model.train()
-        set_probe_mode('reference')           # the reference's train-mode probes (host generator)
+        model.train()                          # probes: --probes (device RNG by default, as in eval)
         params = [p for p in model.parameters() if p.requires_grad]
 
     def step(i):

@@ -234,8 +234,7 @@ class imBlock(nn.Module):
         else:
             z = (self.nnet_x(x0) - self.nnet_z(z_star)) + x0
         if self.training:
-            self.nnet_x_copy.load_state_dict(self.nnet_x.state_dict())
-            self.nnet_z_copy.load_state_dict(self.nnet_z.state_dict())
+            self._refresh_copies()
         z = _ImplicitBackward.apply(z, x, self)
         if logpx is None:
             return z
@@ -366,8 +365,7 @@ class imBlock(nn.Module):
         with torch.no_grad():
             z = self._root(nz, nx, x, self.eps_forward, stream, forward=True)
         if self.training:       # keep the frozen copies in step (implicit_block.py:228-229)
-            self.nnet_x_copy.load_state_dict(self.nnet_x.state_dict())
-            self.nnet_z_copy.load_state_dict(self.nnet_z.state_dict())
+            self._refresh_copies()
         if logpx is None:
             return z
         return z, logpx - self._logdetgrad(z, x)
@@ -409,6 +407,27 @@ class imBlock(nn.Module):
         return x, logpy + self._logdetgrad(z, x)
 
     # ---------------------------------------------------------------------------------------
+    def _refresh_copies(self):
+        """nnet_*_copy.load_state_dict(nnet_*.state_dict()) (implicit_block.py:228-229) as grouped
+        multi-tensor copies: the same values in the same tensors, in a handful of launches instead of one
+        copy per parameter / buffer."""
+        groups = {}
+        for net, cp in ((self.nnet_x, self.nnet_x_copy), (self.nnet_z, self.nnet_z_copy)):
+            src, dst = net.state_dict(keep_vars=True), cp.state_dict(keep_vars=True)
+            for k, t in src.items():
+                d = dst[k]
+                key = (d.device, d.dtype, t.device, t.dtype)
+                g = groups.setdefault(key, ([], []))
+                g[0].append(d)
+                g[1].append(t.detach())
+        with torch.no_grad():
+            for (dd, ddt, sd, sdt), (dsts, srcs) in groups.items():
+                if dd == sd and ddt == sdt and dd.type != 'cpu':
+                    torch._foreach_copy_(dsts, srcs)
+                else:
+                    for a, b in zip(dsts, srcs):
+                        a.copy_(b)
+
     def _host_scalar(self, name, t):
         """t.item() without a device sync per call: re-read only when the tensor changed."""
         key = (t.data_ptr(), t._version, t.device)

@@ -93,3 +93,24 @@ def test_product_path_refuses_cpu_tensors():
     m.load_state_dict(syn.make_state_dict(syn.TOY, 0))
     with pytest.raises(_hip.HipError):
         m(torch.zeros(4, 2), torch.zeros(4, 1))
+
+
+def test_copy_refresh_matches_load_state_dict():
+    """imBlock._refresh_copies (grouped multi-tensor copies) leaves nnet_*_copy equal to what
+    nnet_*_copy.load_state_dict(nnet_*.state_dict()) gives (implicit_block.py:228-229)."""
+    m = build_flow(syn.CIFAR10_SMALL, 2)
+    blk = imblocks(m)[1]
+    torch.manual_seed(3)
+    with torch.no_grad():
+        for t in list(blk.nnet_x.state_dict(keep_vars=True).values()) + \
+                list(blk.nnet_z.state_dict(keep_vars=True).values()):
+            if t.is_floating_point():
+                t.add_(torch.randn_like(t))
+    blk._refresh_copies()
+    for net, cp in ((blk.nnet_x, blk.nnet_x_copy), (blk.nnet_z, blk.nnet_z_copy)):
+        a, b = net.state_dict(), cp.state_dict()
+        assert a.keys() == b.keys()
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    for p in list(blk.nnet_x_copy.parameters()) + list(blk.nnet_z_copy.parameters()):
+        assert not p.requires_grad
