@@ -38,6 +38,7 @@ __all__ = ['imBlock', 'set_probe_mode']
 _PROBES = {'mode': 'reference', 'seed': 0, 'offset': 0}
 
 
+
 def set_probe_mode(mode, seed=0):
     """'reference' (replay the reference's CPU RNG stream) or 'device' (engine RNG)."""
     if mode not in ('reference', 'device'):
@@ -501,7 +502,7 @@ class imBlock(nn.Module):
         """Moment buffers in training (implicit_block.py:345-349); returns (B, 1)."""
         self.last_n_power_series = n_ps
         if self.training and self.n_power_series is None:
-            self.last_n_samples.copy_(torch.as_tensor(np.asarray(ns)).to(self.last_n_samples))
+            solvers.fill_from_host(self.last_n_samples, ns)   # (no pageable H2D copy: it would drain the stream)
             self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
             self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
         return logdetgrad.view(-1, 1)

@@ -19,6 +19,7 @@ from . import solvers
 __all__ = ['iResBlock']
 
 
+
 def _gaussian_probes(x):
     """torch.randn_like(x) (iresblock.py:129).  In the default 'reference' probe mode the draw comes from
     the host generator, so seeded runs replay the reference's CPU stream; 'device' mode draws on the GPU."""
@@ -219,7 +220,7 @@ class iResBlock(nn.Module):
     def _moments(self, logdetgrad, ns):
         """Moment buffers in training (iresblock.py:159-163)."""
         if self.training and self.n_power_series is None and ns is not None:
-            self.last_n_samples.copy_(torch.as_tensor(np.asarray(ns)).to(self.last_n_samples))
+            solvers.fill_from_host(self.last_n_samples, ns)   # (no pageable H2D copy: it would drain the stream)
             self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
             self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
         return logdetgrad

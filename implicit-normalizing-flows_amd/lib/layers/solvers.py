@@ -218,3 +218,15 @@ def surrogate_wJe(net, x, w, vareps):
 def basic_series_graph(net, x, n_power_series, vareps, coeff_fn, training):
     """basic_logdet_estimator with the graph (training with neumann_grad=False, e.g. train_tabular.py)."""
     return basic_logdet_estimator(net(x), x, n_power_series, vareps, coeff_fn, training)
+
+
+def fill_from_host(buf, values):
+    """buf[:] = values (a few host numbers) with device fills: a pageable host-to-device copy is synchronous
+    on ROCm and would drain the stream every training forward (moment buffers, implicit_block.py:345-349)."""
+    vals = np.asarray(values, dtype=np.float64).reshape(-1)
+    flat = buf.view(-1)
+    if vals.size == 1:
+        flat.fill_(float(vals[0]))
+    else:
+        for i in range(min(vals.size, flat.numel())):
+            flat[i].fill_(float(vals[i]))
