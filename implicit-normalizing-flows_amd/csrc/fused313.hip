@@ -627,7 +627,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         if (job < njobs) {
           const int task = job / ksplit, ks = job - task * ksplit;
           const int rb = task / NB, b = task % NB;
-          const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is a multiple of 4
+          const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is even
           // B operand one K tile ahead: its LDS reads and split overlap this tile's MFMA chain
           u32x4 h, m, l;
           if constexpr (PRE_A) bsplit(b, k_lo, h, m, l);
@@ -642,7 +642,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
               cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
             }
           };
-          if constexpr (F_LDS_FLOATS != LDS_HALF) {
+          if (F_LDS_FLOATS != LDS_HALF && (k_hi - k_lo) % 4 == 0) {   // (HID 256 with ksplit 8: 2 K tiles)
             u32x4 r0[3], r1[3], r2[3], r3[3];
             ld3(rb, k_lo, r0);
             ld3(rb, k_lo + 1, r1);
@@ -657,7 +657,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
               if (kt + 6 < k_hi) ld3(rb, kt + 6, r2);
               step(kt + 3, r3);
             }
-          } else {   // 128-VGPR variant: ping-pong only
+          } else {   // 128-VGPR variant, or a K range that is not a multiple of 4 tiles: ping-pong
             u32x4 r0[3], r1[3];
             ld3(rb, k_lo, r0);
             for (int kt = k_lo; kt < k_hi; kt += 2) {
@@ -880,6 +880,9 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool f64 = variant_fits(hid, a0.C, a0.H, a0.W, V64), fh = variant_fits(hid, a0.C, a0.H, a0.W, VHALF);
   int var = f64 ? V64 : (fh ? VHALF : VWIDE);
   if (var == V64 && layout_nets * a0.B * (P / 64) < 256 && fh) var = VHALF;
+  // at most one 32-pixel workgroup per CU anyway: the full-LDS variant (256 VGPRs, deeper operand
+  // prefetch, paired phase-C jobs) beats the two-per-CU one (8x8 scale at B=64: 96 vs 102 us per term)
+  if (var == VHALF && layout_nets * a0.B * (P / 32) <= 256 && variant_fits(hid, a0.C, a0.H, a0.W, VWIDE)) var = VWIDE;
   if (force_bn == 64 && f64) var = V64;
   if (force_bn == 32 && fh) var = VHALF;
   static const int force_var = [] {
