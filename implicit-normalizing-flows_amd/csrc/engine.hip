@@ -124,6 +124,7 @@ struct Bufs {
   std::vector<float*> D;   // saved activation derivatives, one per hidden layer
   float *xin, *xemb, *fx, *xa, *xb, *ga, *gb, *upd, *dx, *dg, *lowest, *va, *vb, *eps_t, *zero, *tmp;
   float *fcur, *flow;      // root solve: f(z) of the latest residual evaluation / of the lowest iterate
+  float* fspec;            // root solve: f(z) of the speculative iteration in flight (broyden_core)
   float *U, *VT;
   float *ext0, *ext1;
   double *part, *bpart, *sumsq;
@@ -153,7 +154,8 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   b.D.resize(n->L.size() > 0 ? n->L.size() - 1 : 0);
   for (auto& p : b.D) p = w.take<float>(Hs);
   float** vecs[] = {&b.xin, &b.xemb, &b.fx, &b.xa, &b.xb, &b.ga, &b.gb, &b.upd,
-                    &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp, &b.fcur, &b.flow};
+                    &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp, &b.fcur, &b.flow,
+                    &b.fspec};
   for (float** v : vecs) *v = w.take<float>(E);
   b.U = w.take<float>((size_t)T * E);
   b.VT = w.take<float>((size_t)T * E);
@@ -354,16 +356,51 @@ int run_vjp(InfNet* n, const float* v, float* vout, const float* xin, const floa
   return n->fc ? launch_fc_out(a, B, s) : launch_conv_out(a, B, s);
 }
 
-// per-sample sums of squares (partials in bf.part) -> host (the reference's .item() per iteration)
-int read_sumsq(InfNet* f, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+// per-sample sums of squares (partials in bf.part) -> host (the reference's .item() per iteration).
+// Asynchronous form: the reduction and a D2H copy into pinned host memory are enqueued and an event marks
+// them; wait_sumsq blocks on that event.  Two slots per host thread let the Broyden loop keep one
+// speculative iteration in flight (broyden_core).  Slots are per thread, so concurrent callers on different
+// threads never share one.
+struct SumsSlot {
+  double* host = nullptr;
+  hipEvent_t ev = nullptr;
+  int cap = 0;
+};
+static int sums_slot(int i, int B, SumsSlot** out) {
+  static thread_local SumsSlot slots[2];
+  SumsSlot& sl = slots[i & 1];
+  if (sl.cap < B) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.host = nullptr;
+    const int cap = std::max(B, 1024);
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sizeof(double) * cap, hipHostMallocDefault) != hipSuccess)
+      return INF_ERR_HIP;
+    sl.cap = cap;
+  }
+  if (!sl.ev && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) return INF_ERR_HIP;
+  *out = &sl;
+  return INF_OK;
+}
+int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
   if (f->fc) {
-    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+    INF_HIP(hipMemcpyAsync(sl->host, bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
   } else {
     INF_TRY(launch_reduce_partials(bf.part, B, bf.nchunk, bf.sumsq, s));
-    INF_HIP(hipMemcpyAsync(host_sumsq.data(), bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+    INF_HIP(hipMemcpyAsync(sl->host, bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
   }
-  INF_HIP(hipStreamSynchronize(s));
+  INF_HIP(hipEventRecord(sl->ev, s));
   return INF_OK;
+}
+int wait_sumsq(SumsSlot* sl, int B, std::vector<double>& host_sumsq) {
+  INF_HIP(hipEventSynchronize(sl->ev));
+  memcpy(host_sumsq.data(), sl->host, sizeof(double) * B);
+  return INF_OK;
+}
+int read_sumsq(InfNet* f, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+  SumsSlot* sl = nullptr;
+  INF_TRY(sums_slot(0, B, &sl));
+  INF_TRY(enqueue_sumsq(f, B, bf, sl, s));
+  return wait_sumsq(sl, B, host_sumsq);
 }
 
 // residual evaluation g = x_embed - f(z) - z (+ dg = g - g_prev) and per-sample sum of squares -> host
@@ -383,14 +420,28 @@ int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, 
   INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
   return read_sumsq(f, B, bf, host_sumsq, s);
 }
+int eval_resid_async(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
+                     const float* gprev, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = xemb;
+  a.in1 = zsub;
+  a.in2 = gprev;
+  a.out0 = gout;
+  a.out1 = dg;
+  a.out2 = bf.fcur;
+  a.partial = bf.part;
+  a.nchunk = bf.nchunk;
+  INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
+  return enqueue_sumsq(f, B, bf, sl, s);
+}
 
 // vjp residual of the implicit backward (implicit_block.py:186-190): g = (y + y^T J) - grad
-int vjp_resid(InfNet* f, const float* y, const float* zi, const float* gradi, float* gout, float* dg,
-              const float* gprev, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
+int vjp_resid_async(InfNet* f, const float* y, const float* zi, const float* gradi, float* gout, float* dg,
+                    const float* gprev, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
   INF_TRY(run_vjp(f, y, bf.tmp, zi, nullptr, nullptr, B, bf, s));
   INF_TRY(launch_vjp_resid(bf.tmp, y, gradi, gprev, gout, dg, bf.part, B, f->d, f->fc ? 1 : bf.nchunk, f->fc, s));
-  return read_sumsq(f, B, bf, host_sumsq, s);
-  return INF_OK;
+  return enqueue_sumsq(f, B, bf, sl, s);
 }
 
 double total(const std::vector<double>& v) {
@@ -420,8 +471,8 @@ bool same_shape(const InfNet* a, const InfNet* b) {
 // Broyden root find on internal-layout buffers.  Solves z with g(z) = xemb - f(z) - z = 0.
 // Result (lowest iterate) in bf.lowest.  y (internal) is the Banach fallback start.
 // residual g(x) -> gout (+ dg = g - gprev when gprev), per-sample sums of squares -> host
-using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev,
-                                  std::vector<double>& host_sumsq)>;
+// (enqueue only: the per-sample sums of squares land in the slot, wait_sumsq retrieves them)
+using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev, SumsSlot* sl)>;
 
 // broyden.py:123-193 with the residual as a callback; the result (lowest iterate) is in bf.lowest.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
@@ -435,69 +486,39 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   memset(&stats, 0, sizeof(stats));
   stats.eps = eps;
 
-  // Iterates rotate through three buffers {xa, xb, lowest} and f(z) through two {fcur, flow}: the lowest
-  // iterate (and its f) is tracked by pointer instead of copied every time it improves (broyden.py:159-162);
-  // the Bufs pointers are permuted at the end so that bf.lowest / bf.flow name the result.
+  // One iteration of lookahead: while the host waits for iteration k's residual norm (the reference's
+  // .item(), broyden.py:157), iteration k+1's low-rank update and residual are already queued behind it, so
+  // the GPU does not idle through the host round trip.  If k stops the loop, k+1's work is discarded: it
+  // only wrote scratch.  Iterates rotate through {xa, xb, lowest} and f(z) through {fcur, flow, fspec}: the
+  // decided lowest, the pending and the speculative one are always distinct buffers; the lowest iterate
+  // (broyden.py:159-162) is tracked by pointer and the Bufs pointers are permuted at the end so that
+  // bf.lowest / bf.flow name the result.
   float* xpool[3] = {bf.xa, bf.xb, bf.lowest};
-  float* fpool[2] = {bf.fcur, bf.flow};
-  float *x = xpool[0], *xn = xpool[1], *gx = bf.ga, *gn = bf.gb;
-  float *low = x, *flow = fpool[1];
-  auto free_x = [&]() {
-    for (float* p : xpool)
-      if (p != x && p != low) return p;
-    return xpool[0];
+  float* fpool[3] = {bf.fcur, bf.flow, bf.fspec};
+  auto pick = [](float* const* pool, const float* a, const float* b) {
+    for (int i = 0; i < 3; ++i)
+      if (pool[i] != a && pool[i] != b) return pool[i];
+    return pool[0];
   };
-  auto next_f = [&]() { bf.fcur = (flow == fpool[0]) ? fpool[1] : fpool[0]; };
-  next_f();
+  SumsSlot* slot[2];
+  INF_TRY(sums_slot(0, B, &slot[0]));
+  INF_TRY(sums_slot(1, B, &slot[1]));
+  float *gx = bf.ga, *gn = bf.gb;
+  float* x = xpool[0];
+  float *low = x, *flow = nullptr;
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
   INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
-  INF_TRY(resid(x, gx, nullptr, nullptr, ss));
+  bf.fcur = fpool[0];
+  INF_TRY(resid(x, gx, nullptr, nullptr, slot[0]));
+  INF_TRY(wait_sumsq(slot[0], B, ss));
   const double init = sqrt(total(ss));
   double obj = init, lowest = init;
   lowest_ss = ss;
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
-  low = x;
-  if (keep_f) {
-    flow = bf.fcur;
-    next_f();
-  }
-  xn = free_x();
-  // update = -gx; x_est = x0 + update
-  INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
-  INF_TRY(launch_axpy_step(x, bf.upd, xn, bf.dx, (long)E, s));
-  while (obj >= eps && nstep < T) {                                   // broyden.py:153
-    INF_TRY(resid(xn, gn, bf.dg, gx, ss));
-    std::swap(x, xn);
-    std::swap(gx, gn);
-    nstep += 1;
-    obj = sqrt(total(ss));
-    trace.push_back(obj);
-    if (obj < lowest) {                                               // :159-162
-      low = x;
-      if (keep_f) {
-        flow = bf.fcur;
-        next_f();
-      }
-      lowest = obj;
-      lowest_step = nstep;
-      lowest_ss = ss;
-    }
-    if (obj < eps) break;
-    if (obj < 3 * eps && nstep == T) {                                // :165-168
-      const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
-      double mx = trace[k0], mn = trace[k0];
-      for (size_t k = k0; k < trace.size(); ++k) {
-        mx = std::max(mx, trace[k]);
-        mn = std::min(mn, trace[k]);
-      }
-      if (mx / mn < 1.3) break;
-    }
-    if (obj > init * 1e6) {                                           // :169-172
-      stats.prot_break = 1;
-      break;
-    }
+  if (keep_f) flow = bf.fcur;
+  auto update = [&](float* xfrom, float* gfrom, float* xto) {          // broyden.py:174-181
     BroydenArgs ba;
     memset(&ba, 0, sizeof(ba));
     ba.batch = B;
@@ -510,17 +531,71 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     ba.VT = bf.VT;
     ba.dx = bf.dx;
     ba.dg = bf.dg;
-    ba.gx = gx;
-    ba.x = x;
-    ba.xnew = xn;
+    ba.gx = gfrom;
+    ba.x = xfrom;
+    ba.xnew = xto;
     ba.dxnew = bf.dx;
     ba.upd = bf.upd;
     ba.part = bf.bpart;
     ba.m = (nstep - 1) % T;
     ba.ncols = std::min(nstep, T);
-    xn = free_x();
-    ba.xnew = xn;
-    INF_TRY(launch_broyden_update(ba, s));
+    return launch_broyden_update(ba, s);
+  };
+  if (obj >= eps && nstep < T) {                                      // broyden.py:153
+    // pending iteration 1: update = -g0, x1 = x0 + update (:144), its residual
+    float* xp = pick(xpool, low, nullptr);
+    INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
+    INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
+    float* fp = pick(fpool, flow, nullptr);
+    bf.fcur = fp;
+    INF_TRY(resid(xp, gn, bf.dg, gx, slot[1]));
+    int ps = 1;
+    for (;;) {
+      // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps]);
+      // speculate iteration nstep + 2 when the threshold allows it
+      const bool spec = nstep + 1 < T;
+      float *xs = nullptr, *fs = nullptr;
+      if (spec) {
+        nstep += 1;                                  // the update's column index is that of the pending step
+        xs = pick(xpool, low, xp);
+        INF_TRY(update(xp, gn, xs));
+        nstep -= 1;
+        fs = pick(fpool, flow, fp);
+        bf.fcur = fs;
+        INF_TRY(resid(xs, gx, bf.dg, gn, slot[1 - ps]));
+      }
+      INF_TRY(wait_sumsq(slot[ps], B, ss));
+      nstep += 1;
+      x = xp;
+      obj = sqrt(total(ss));
+      trace.push_back(obj);
+      if (obj < lowest) {                                               // :159-162
+        low = xp;
+        if (keep_f) flow = fp;
+        lowest = obj;
+        lowest_step = nstep;
+        lowest_ss = ss;
+      }
+      if (obj < eps) break;
+      if (obj < 3 * eps && nstep == T) {                                // :165-168
+        const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
+        double mx = trace[k0], mn = trace[k0];
+        for (size_t k = k0; k < trace.size(); ++k) {
+          mx = std::max(mx, trace[k]);
+          mn = std::min(mn, trace[k]);
+        }
+        if (mx / mn < 1.3) break;
+      }
+      if (obj > init * 1e6) {                                           // :169-172
+        stats.prot_break = 1;
+        break;
+      }
+      if (!spec) break;                                                 // nstep == T
+      xp = xs;
+      fp = fs;
+      ps = 1 - ps;
+      std::swap(gx, gn);                                                // gn: the new pending residual
+    }
   }
   // name the result: bf.lowest = the lowest iterate, bf.flow = its f; the other buffers become scratch
   {
@@ -531,8 +606,14 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     bf.lowest = low;
     bf.xa = rest[0];
     bf.xb = rest[1];
-    bf.flow = flow;
-    bf.fcur = (flow == fpool[0]) ? fpool[1] : fpool[0];
+    float* fr[2];
+    k = 0;
+    const float* fl = flow ? flow : fpool[1];
+    for (float* p : fpool)
+      if (p != fl && k < 2) fr[k++] = p;
+    bf.flow = const_cast<float*>(fl);
+    bf.fcur = fr[0];
+    bf.fspec = fr[1];
   }
   stats.nstep = nstep;
   stats.lowest_step = lowest_step;
@@ -564,13 +645,13 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   std::vector<double> lowest_ss;
   INF_TRY(ensure_f0(f, B, bf, s));
   bool first = !f->fc;           // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached
-  const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
+  const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, SumsSlot* sl) {
     if (first) {
       first = false;
       INF_TRY(launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s));
-      return read_sumsq(f, B, bf, ss, s);
+      return enqueue_sumsq(f, B, bf, sl, s);
     }
-    return eval_resid(f, x, x, bf.xemb, gout, dg, gprev, B, bf, ss, s);
+    return eval_resid_async(f, x, x, bf.xemb, gout, dg, gprev, B, bf, sl, s);
   };
   INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
   if (diff_detail) {
@@ -1099,8 +1180,8 @@ int inf_imblock_backward(InfNet* nx, InfNet* nz, const float* z, const float* x,
     INF_TRY(run_forward(nz, zi, B, bf, -1, nullptr, s));      // activation derivatives at z
     InfBroydenStats bs;
     std::vector<double> lowest_ss;
-    const ResidFn resid = [&](const float* y, float* gout, float* dg, const float* gprev, std::vector<double>& ss) {
-      return vjp_resid(nz, y, zi, gi, gout, dg, gprev, B, bf, ss, s);
+    const ResidFn resid = [&](const float* y, float* gout, float* dg, const float* gprev, SumsSlot* sl) {
+      return vjp_resid_async(nz, y, zi, gi, gout, dg, gprev, B, bf, sl, s);
     };
     INF_TRY(broyden_core(nz, resid, B, T, eps, bs, lowest_ss, bf, s));
     if (stats) *stats = bs;
