@@ -110,7 +110,7 @@ def test_copy_refresh_matches_load_state_dict():
     for net, cp in ((blk.nnet_x, blk.nnet_x_copy), (blk.nnet_z, blk.nnet_z_copy)):
         a, b = net.state_dict(), cp.state_dict()
         assert a.keys() == b.keys()
-        for k in a:
-            assert torch.equal(a[k], b[k]), k
+        for k in a:   # (some buffers are torch.empty until first use: compare NaN-aware, bit for bit)
+            torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, equal_nan=True, msg=k)
     for p in list(blk.nnet_x_copy.parameters()) + list(blk.nnet_z_copy.parameters()):
         assert not p.requires_grad
