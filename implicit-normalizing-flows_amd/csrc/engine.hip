@@ -511,13 +511,24 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
   bf.fcur = fpool[0];
   INF_TRY(resid(x, gx, nullptr, nullptr, slot[0]));
+  if (keep_f) flow = bf.fcur;
+  // iteration 1 is queued before the initial norm is read (update = -g0, x1 = x0 + update, :144)
+  float* xp = nullptr;
+  float* fp = nullptr;
+  if (T > 0) {
+    xp = pick(xpool, low, nullptr);
+    INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
+    INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
+    fp = pick(fpool, flow, nullptr);
+    bf.fcur = fp;
+    INF_TRY(resid(xp, gn, bf.dg, gx, slot[1]));
+  }
   INF_TRY(wait_sumsq(slot[0], B, ss));
   const double init = sqrt(total(ss));
   double obj = init, lowest = init;
   lowest_ss = ss;
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
-  if (keep_f) flow = bf.fcur;
   auto update = [&](float* xfrom, float* gfrom, float* xto) {          // broyden.py:174-181
     BroydenArgs ba;
     memset(&ba, 0, sizeof(ba));
@@ -542,13 +553,6 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     return launch_broyden_update(ba, s);
   };
   if (obj >= eps && nstep < T) {                                      // broyden.py:153
-    // pending iteration 1: update = -g0, x1 = x0 + update (:144), its residual
-    float* xp = pick(xpool, low, nullptr);
-    INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
-    INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
-    float* fp = pick(fpool, flow, nullptr);
-    bf.fcur = fp;
-    INF_TRY(resid(xp, gn, bf.dg, gx, slot[1]));
     int ps = 1;
     for (;;) {
       // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps]);
