@@ -1211,12 +1211,17 @@ int inf_imblock_backward(InfNet* nx, InfNet* nz, const float* z, const float* x,
 // directly (tap sum, preact swish', trace partial -- conv_out's work), so a term is ONE launch; only
 // the last term's taps go through conv_out.  Series slabs: part[k][b][snchunk] (zeroed first: the
 // fused kernel fills one entry per tile, conv_out one per 1024-element chunk).
+// Neumann mode (wouts != nullptr, ncoeff a host array of n_terms + 1): instead of the trace partials, each
+// term's staging accumulates w += ncoeff[k] v_k for its own pixels (w starts as eps, the last term's taps go
+// through conv_out), i.e. the Neumann vector of implicit_block.py:430-436 for 1 or 2 nets in lockstep.
 int series_fused(InfNet* const* nets, const float* const* xs, const float* const* es, int nn, const float* coeff,
-                 int n_terms, float* const* outs, int B, Bufs* bfs, hipStream_t s, unsigned save_mask = 3u) {
+                 int n_terms, float* const* outs, int B, Bufs* bfs, hipStream_t s, unsigned save_mask = 3u,
+                 float* const* wouts = nullptr, const float* ncoeff = nullptr) {
   Net313Args args[2];
   for (int i = 0; i < nn; ++i) {
     args[i] = net313_args(nets[i], xs[i], B, bfs[i], false);
-    INF_HIP(hipMemsetAsync(bfs[i].part, 0, sizeof(double) * n_terms * B * bfs[i].snchunk, s));
+    if (!wouts) INF_HIP(hipMemsetAsync(bfs[i].part, 0, sizeof(double) * n_terms * B * bfs[i].snchunk, s));
+    else INF_HIP(hipMemcpyAsync(wouts[i], es[i], sizeof(float) * (size_t)B * nets[i]->d, hipMemcpyDeviceToDevice, s));
   }
   // activation derivatives (in the pair's tile layout); a net whose d1/d2 are already saved is skipped
   const unsigned all = (1u << nn) - 1u;
@@ -1238,12 +1243,39 @@ int series_fused(InfNet* const* nets, const float* const* xs, const float* const
         v.in_taps = (k % 2 == 1) ? bf.Y : bf.Y2;
         v.vmul_x = n->pre_beta ? xs[i] : nullptr;
         v.vmul_beta = n->pre_beta;
-        v.dot_eps = es[i];
-        v.dot_part = bf.part + (size_t)(k - 1) * B * bf.snchunk;
-        v.dot_nchunk = bf.snchunk;
+        if (wouts) {
+          v.acc_w = wouts[i];
+          v.acc_coef = ncoeff[k];
+        } else {
+          v.dot_eps = es[i];
+          v.dot_part = bf.part + (size_t)(k - 1) * B * bf.snchunk;
+          v.dot_nchunk = bf.snchunk;
+        }
       }
     }
     INF_TRY(launch_net313_multi(args, nn, nets[0]->fhid, MODE_VJP, s));
+  }
+  if (wouts) {
+    for (int i = 0; i < nn; ++i) {
+      InfNet* n = nets[i];
+      Bufs& bf = bfs[i];
+      OutArgs a;
+      memset(&a, 0, sizeof(a));
+      a.Y = ((n_terms - 1) % 2 == 0) ? bf.Y : bf.Y2;
+      a.y_sample = (long)n->M3 * n->P;
+      a.C = n->C;
+      a.H = n->H;
+      a.W = n->W;
+      a.ks = 3;
+      a.mode = OM_VJP;
+      a.in1 = xs[i];
+      a.out0 = bf.va;
+      a.pre_beta = n->pre_beta;
+      a.nchunk = bf.snchunk;
+      INF_TRY(launch_conv_out(a, B, s));
+      INF_TRY(glue_axpy_scaled(wouts[i], bf.va, ncoeff[n_terms], (long)B * n->d, s));
+    }
+    return INF_OK;
   }
   for (int i = 0; i < nn; ++i) {
     InfNet* n = nets[i];
@@ -1473,6 +1505,32 @@ int inf_neumann_vector(InfNet* n, const float* x, const float* vareps, const flo
   INF_TRY(st);
   INF_TRY(neumann_w(n, xi, ei, ncoeff, n_terms, B, bf, s));
   return to_boundary(n, bf.tmp, w, B, s);
+}
+
+// Both nets' Neumann vectors (x- and z-branch of an imBlock's training log-det) in lockstep: one fused VJP
+// launch per term for both nets with the accumulation folded into the next term's staging.  Nets off the
+// fused path (or n_terms == 0) fall back to two inf_neumann_vector computations.
+int inf_neumann_vector_pair(InfNet* na, const float* xa, const float* ea, InfNet* nb, const float* xb,
+                            const float* eb, const float* ncoeff, int n_terms, float* wa, float* wb, int B, void* ws,
+                            size_t ws_bytes, void* stream) {
+  if (!na || !nb || !xa || !xb || !ea || !eb || !ncoeff || !wa || !wb || B <= 0 || n_terms < 0 || !same_shape(na, nb))
+    return INF_ERR_INVALID;
+  const size_t half = ws_bytes / 2;
+  if (!(na->fused && nb->fused && na->fhid == nb->fhid) || n_terms == 0) {
+    INF_TRY(inf_neumann_vector(na, xa, ea, ncoeff, n_terms, wa, B, ws, half, stream));
+    return inf_neumann_vector(nb, xb, eb, ncoeff, n_terms, wb, B, reinterpret_cast<char*>(ws) + half, half, stream);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bfs[2];
+  if (!ws || carve(na, B, 1, ws, half, bfs[0]) > half ||
+      carve(nb, B, 1, reinterpret_cast<char*>(ws) + half, half, bfs[1]) > half)
+    return INF_ERR_WORKSPACE;
+  InfNet* nets[2] = {na, nb};
+  const float* xs[2] = {xa, xb};
+  const float* es[2] = {ea, eb};
+  float* wouts[2] = {wa, wb};
+  float* outs[2] = {nullptr, nullptr};
+  return series_fused(nets, xs, es, 2, nullptr, n_terms, outs, B, bfs, s, 3u, wouts, ncoeff);
 }
 
 int inf_logdet_neumann(InfNet* n, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* out,

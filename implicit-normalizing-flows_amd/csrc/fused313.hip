@@ -175,9 +175,11 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     // compiler fuse each slot's loads with their use), so a small halo costs one pass of 11 loads.
     const float* mxp = mx ? mx : ytap;
     const float* epp = ep ? ep : ytap;
+    float* accw = a.acc_w ? a.acc_w + (long)img * a.C * P : nullptr;   // Neumann-vector accumulator
+    const float* awp = accw ? accw : ytap;
     auto pass = [&](auto nuc, int i0) {
       constexpr int NU = decltype(nuc)::value;
-      float tv[NU][9], xm[NU], ev[NU];
+      float tv[NU][9], xm[NU], ev[NU], wv[NU];
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int i = i0 + u * NT;
@@ -194,6 +196,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         }
         xm[u] = mxp[ee];
         ev[u] = epp[ee];
+        wv[u] = awp[ee];
       }
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
@@ -214,6 +217,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         if (mx) v = v * swish_d(xm[u], msp);
         v = ok ? v : 0.f;
         if (ep && ok == 2) dacc += (double)v * (double)ev[u];
+        if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
         if (i < vhz) vh[i] = v;
       }
     };

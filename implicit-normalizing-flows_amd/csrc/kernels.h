@@ -154,6 +154,8 @@ struct Net313Args {
   const float* dot_eps;   // with in_taps: dot_part[img * dot_nchunk + tile] = sum over the tile's own
   double* dot_part;       //   pixels of v * dot_eps (fp64), the previous term's trace partial
   int dot_nchunk;
+  float* acc_w;           // with in_taps: acc_w[img, own pixels] += acc_coef * v (Neumann vector accumulation,
+  float acc_coef;         //   implicit_block.py:430-436), v the previous term's VJP after the tap sum
 };
 struct Net313Pair {
   Net313Args a[2];

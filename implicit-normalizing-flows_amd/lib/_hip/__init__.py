@@ -99,6 +99,8 @@ _SIGS = {
                                           ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_neumann_vector': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                           ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_neumann_vector_pair': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                               _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact': (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_exact_trace': (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, ctypes.c_int,
                                               _P, ctypes.c_size_t, _P]),

@@ -272,10 +272,12 @@ class imBlock(nn.Module):
         nx, nz, stream = self._native(x)
         ests = []
         engine = self._engine_grads(x)
-        for net, native, t, eps in ((self.nnet_x, nx, x, vareps_x), (self.nnet_z, nz, z, vareps_z)):
-            if neumann and engine and self.training and self.grad_in_forward:
-                w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
-                ests.append(_MemEffNeumannNative.apply(t, native, net, w, eps, *list(net.parameters())))
+        native_neumann = neumann and engine and self.training and self.grad_in_forward
+        if native_neumann:        # both branches' Neumann vectors in lockstep (one fused launch per term)
+            ws_pair = self._neumann_pair(nx, x.detach(), vareps_x, nz, z.detach(), vareps_z, n_ps, coeff_fn, stream)
+        for i, (net, native, t, eps) in enumerate(((self.nnet_x, nx, x, vareps_x), (self.nnet_z, nz, z, vareps_z))):
+            if native_neumann:
+                ests.append(_MemEffNeumannNative.apply(t, native, net, ws_pair[i], eps, *list(net.parameters())))
                 continue
             if neumann:
                 w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
@@ -316,6 +318,27 @@ class imBlock(nn.Module):
         _hip.check(_hip.load().inf_net_forward(native.handle, _hip.ptr(t.contiguous()), _hip.ptr(y), B, _hip.ptr(ws),
                                                ws.numel(), _hip.stream_of(t)), 'inf_net_forward')
         return y
+
+    @staticmethod
+    def _neumann_coeffs(n_ps, coeff_fn):
+        nco = np.zeros(n_ps + 1, dtype=np.float32)
+        nco[0] = 1.
+        for k in range(1, n_ps + 1):
+            nco[k] = (-1) ** k * coeff_fn(k)
+        return nco
+
+    def _neumann_pair(self, na, ta, ea, nb, tb, eb, n_ps, coeff_fn, stream):
+        """neumann_vjp (implicit_block.py:430-436) of both branches: inf_neumann_vector_pair."""
+        B = ta.shape[0]
+        nco = self._neumann_coeffs(n_ps, coeff_fn)
+        wa, wb = torch.empty_like(ta), torch.empty_like(tb)
+        ws = _hip.workspace(ta.device, 2 * max(na.ws_bytes(B), nb.ws_bytes(B)))
+        half = ws.numel() // 2
+        _hip.check(_hip.load().inf_neumann_vector_pair(
+            na.handle, _hip.ptr(ta.contiguous()), _hip.ptr(ea), nb.handle, _hip.ptr(tb.contiguous()), _hip.ptr(eb),
+            nco.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(wa), _hip.ptr(wb), B, _hip.ptr(ws),
+            2 * half, stream), 'inf_neumann_vector_pair')
+        return wa, wb
 
     def _neumann_vector(self, native, t, eps, n_ps, coeff_fn, stream):
         B = t.shape[0]

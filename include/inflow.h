@@ -150,6 +150,11 @@ int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const f
  * implicit_block.py:430-436), for the training surrogate's gradient. */
 int inf_neumann_vector(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms, float* w,
                        int batch, void* ws, size_t ws_bytes, void* stream);
+/* Both Neumann vectors of an imBlock (x-branch at x with eps_a, z-branch at z with eps_b) in lockstep: one
+ * fused VJP launch per term for both nets.  ws >= 2 x inf_workspace_bytes(net, batch, 1). */
+int inf_neumann_vector_pair(InfNet* net_a, const float* x_a, const float* vareps_a, InfNet* net_b, const float* x_b,
+                            const float* vareps_b, const float* ncoeff, int n_terms, float* w_a, float* w_b,
+                            int batch, void* ws, size_t ws_bytes, void* stream);
 /* Exact log|det(I + J_nnet(x))| for fc nets with d <= 16 (implicit_block.py:249-260,358-362). */
 int inf_logdet_exact(InfNet* net, const float* x, float* out, int batch, void* ws, size_t ws_bytes, void* stream);
 /* Implicit backward of an imBlock (imBlock.Backward, implicit_block.py:165-217): given dL/dz = grad, solve
