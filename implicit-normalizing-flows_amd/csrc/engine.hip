@@ -185,6 +185,7 @@ size_t ws_need(const InfNet* n, int B, int T) {
 GemmArgs gemm_base(const InfNet* n, const Operand& op, const float* X, int in_ch, int B) {
   GemmArgs g;
   memset(&g, 0, sizeof(g));
+  g.x6 = n->mfma_mode == INF_MFMA_BF16X6;
   g.A = op.A;
   g.M = op.M;
   g.Kpad = op.Kpad;

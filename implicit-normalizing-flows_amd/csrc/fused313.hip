@@ -51,57 +51,6 @@ __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = v1.w;
 }
 
-// ---- split-bf16 ("x6") contraction: fp32-level products at the bf16 MFMA rate ----------------------
-// x = hi + mid + lo exactly (truncation: hi = top 16 bits, mid = top 16 bits of x - hi, lo = the rest,
-// which has <= 8 significant bits).  x.w ~ hh + hm + mh + hl + lh + mm; the dropped ml, lm, ll terms are
-// <= ~2^-23 |x||w|, the size of fp32's own rounding.  v_mfma_f32_32x32x16_bf16 takes the same k-slots per
-// lane as 8 consecutive v_mfma_f32_32x32x2_f32 steps (lane l: row/column l&31, k = 8 (l>>5) + 0..7), so
-// the fragment-major layouts carry over unchanged: 6 bf16 MFMAs (32 cycles each) replace 8 fp32 ones
-// (64 cycles each).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split3(const float (&x)[8], u32x4& h, u32x4& m, u32x4& l) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const unsigned u0 = __float_as_uint(x[2 * j]), u1 = __float_as_uint(x[2 * j + 1]);
-#ifdef INFLOW_SPLIT_PK
-    const f32x2 xv = {x[2 * j], x[2 * j + 1]};
-    const f32x2 hv = {__uint_as_float(u0 & 0xffff0000u), __uint_as_float(u1 & 0xffff0000u)};
-    const f32x2 r = xv - hv;                                  // v_pk_add_f32 (exact)
-    const unsigned v0 = __float_as_uint(r.x), v1 = __float_as_uint(r.y);
-    const f32x2 mv = {__uint_as_float(v0 & 0xffff0000u), __uint_as_float(v1 & 0xffff0000u)};
-    const f32x2 sl = r - mv;                                  // exact, <= 8 significant bits
-    const float s0 = sl.x, s1 = sl.y;
-#else
-    const float r0 = x[2 * j] - __uint_as_float(u0 & 0xffff0000u);       // exact
-    const float r1 = x[2 * j + 1] - __uint_as_float(u1 & 0xffff0000u);
-    const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
-    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);             // exact, <= 8 significant bits
-    const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
-#endif
-    h[j] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-    m[j] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
-    l[j] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);
-  }
-}
-__device__ __forceinline__ f32x16 mfma_bf16(const u32x4& a, const u32x4& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                 0, 0, 0);
-}
-// acc += A.B with A = (a[0], a[1], a[2]) pre-split planes, B = (h, m, l); small terms first
-__device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4& h, const u32x4& m, const u32x4& l,
-                                         f32x16 c) {
-  c = mfma_bf16(a[0], l, c);
-  c = mfma_bf16(a[2], h, c);
-  c = mfma_bf16(a[1], m, c);
-  c = mfma_bf16(a[0], m, c);
-  c = mfma_bf16(a[1], h, c);
-  c = mfma_bf16(a[0], h, c);
-  return c;
-}
-
 // fragment-major offset of (row block rb, k tile kt) for a matrix with nkt K tiles
 __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;

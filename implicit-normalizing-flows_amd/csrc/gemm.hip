@@ -219,6 +219,23 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs g) {
       af[a][0] = v0.x; af[a][1] = v0.y; af[a][2] = v0.z; af[a][3] = v0.w;
       af[a][4] = v1.x; af[a][5] = v1.y; af[a][6] = v1.z; af[a][7] = v1.w;
     }
+    if (g.x6) {
+      // split-bf16: the 16-deep tile as 6 bf16 MFMAs per (a, b) (the lane's k-slots of the two operands are
+      // those of the 8 f32 steps below, so the LDS images are unchanged)
+      u32x4 as[TM][3];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) split3(af[a], as[a][0], as[a][1], as[a][2]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        float bx[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) bx[kk] = Bs[cur][(lh * 8 + kk) * BN + wn * TN * 32 + b * 32 + li];
+        u32x4 bh, bm, bl;
+        split3(bx, bh, bm, bl);
+#pragma unroll
+        for (int a = 0; a < TM; ++a) acc[a][b] = mfma_x6(as[a], bh, bm, bl, acc[a][b]);
+      }
+    } else
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       float bf[TN];

@@ -32,6 +32,7 @@ struct GemmArgs {
   int write_out;          // EP_BIAS_ACT: write act(a)
   const float* deriv_in;  // EP_MUL_DERIV multiplier (same indexing as out)
   int n_primal;           // EP_BIAS_PRIMAL: columns n < n_primal get the bias
+  int x6;                 // 1: split-bf16 MFMA (both operands split exactly into 3 bf16 pieces, common.h)
 };
 int launch_gemm(const GemmArgs& g, int bload, int epi, hipStream_t s);
 
