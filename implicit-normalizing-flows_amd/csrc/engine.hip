@@ -530,7 +530,8 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   lowest_ss = ss;
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
-  auto update = [&](float* xfrom, float* gfrom, float* xto) {          // broyden.py:174-181
+  // low-rank update from iterate `step` (x = xfrom, g = gfrom) to xto (broyden.py:174-181)
+  auto update = [&](int step, float* xfrom, float* gfrom, float* xto) {
     BroydenArgs ba;
     memset(&ba, 0, sizeof(ba));
     ba.batch = B;
@@ -549,29 +550,33 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     ba.dxnew = bf.dx;
     ba.upd = bf.upd;
     ba.part = bf.bpart;
-    ba.m = (nstep - 1) % T;
-    ba.ncols = std::min(nstep, T);
+    ba.m = (step - 1) % T;
+    ba.ncols = std::min(step, T);
     return launch_broyden_update(ba, s);
   };
   if (obj >= eps && nstep < T) {                                      // broyden.py:153
     int ps = 1;
+    double prev_obj = -1.0;
     for (;;) {
-      // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps]);
-      // speculate iteration nstep + 2 when the threshold allows it
-      const bool spec = nstep + 1 < T;
+      // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps]).  The next
+      // iteration is queued before the pending norm is read, unless the threshold forbids it or the
+      // observed contraction predicts that the pending iteration converges (then it would be wasted work).
+      const bool allow = nstep + 1 < T;
+      const bool likely_last = prev_obj > 0.0 && obj * (obj / prev_obj) < eps;
       float *xs = nullptr, *fs = nullptr;
-      if (spec) {
-        nstep += 1;                                  // the update's column index is that of the pending step
+      auto enqueue_next = [&](int pending_step) -> int {
         xs = pick(xpool, low, xp);
-        INF_TRY(update(xp, gn, xs));
-        nstep -= 1;
+        INF_TRY(update(pending_step, xp, gn, xs));
         fs = pick(fpool, flow, fp);
         bf.fcur = fs;
-        INF_TRY(resid(xs, gx, bf.dg, gn, slot[1 - ps]));
-      }
+        return resid(xs, gx, bf.dg, gn, slot[1 - ps]);
+      };
+      const bool spec = allow && !likely_last;
+      if (spec) INF_TRY(enqueue_next(nstep + 1));
       INF_TRY(wait_sumsq(slot[ps], B, ss));
       nstep += 1;
       x = xp;
+      prev_obj = obj;
       obj = sqrt(total(ss));
       trace.push_back(obj);
       if (obj < lowest) {                                               // :159-162
@@ -595,7 +600,8 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
         stats.prot_break = 1;
         break;
       }
-      if (!spec) break;                                                 // nstep == T
+      if (!allow) break;                                                // nstep == T
+      if (!spec) INF_TRY(enqueue_next(nstep));
       xp = xs;
       fp = fs;
       ps = 1 - ps;
