@@ -708,7 +708,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
 // ---------------------------------------------------------------------------------------------
 struct GradBufs {
   std::vector<float*> H, Hd, Ad;     // pre-activations, their tangents, activation tangents (Ad[0]: input)
-  float *gA, *gB, *hA, *hB, *gad, *ga, *Y, *slab, *dWe, *dWe2, *dsig, *xin, *tmp_in;
+  float *gA, *gB, *hA, *hB, *gad, *ga, *Y, *slab, *dWe, *dWe2, *dsig, *xin, *tmp_in, *act;
   double *bpart, *dot;
   int max_split;
 };
@@ -735,6 +735,7 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
   g.dsig = w.take<float>(mn);
   g.xin = w.take<float>(in);
   g.tmp_in = w.take<float>(in);
+  g.act = w.take<float>(std::max(hid, in));   // swish of a stored pre-activation (weight-gradient operand)
   g.bpart = w.take<double>(std::max<size_t>(GRAD_BLOCKS + 64, glue_batched_dot_scratch(B, (long)n->hidden_max * n->P) + 64));
   g.dot = w.take<double>(128);      // [0] the dot, [1..64] its block partials
   g.max_split = GRAD_SPLIT;
@@ -841,6 +842,16 @@ static int layer_param_grads(InfNet* n, int l, const float* G_tan, const float* 
   float* dW = grad_out(gr->dW, l);
   if (dW) {
     const long mn = (long)w.cout * w.cin * w.ks * w.ks;
+    // the primal operand's swish once per element (INFLOW_WGRAD_PREACT=0: inside the wgrad loaders)
+    static const bool pre_act = [] {
+      const char* e = getenv("INFLOW_WGRAD_PREACT");
+      return !(e && e[0] == '0');
+    }();
+    if (pre_act && G_pri && X_pri_beta) {
+      INF_TRY(launch_swish_apply(X_pri, X_pri_beta, gb.act, (long)B * w.cin * n->P, s));
+      X_pri = gb.act;
+      X_pri_beta = nullptr;
+    }
     if (G_tan) {
       INF_TRY(layer_wgrad(n, l, G_tan, X_tan, nullptr, gb.dWe, B, gb, s));
       if (G_pri) {

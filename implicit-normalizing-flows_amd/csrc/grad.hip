@@ -438,6 +438,17 @@ int launch_act_bwd1(const float* ga, const float* h, const float* beta, float* g
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
+// out = swish(h) (activations.py:64-71), once per element: the weight-gradient operand of a layer whose input
+// is the swish of a stored pre-activation (the wgrad loaders would otherwise recompute it per output tile)
+__global__ void swish_apply_kernel(const float* h, const float* beta, float* out, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = swish_f(h[i], softplus_f(*beta));
+}
+int launch_swish_apply(const float* h, const float* beta, float* out, long n, hipStream_t s) {
+  hipLaunchKernelGGL(swish_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, h, beta, out, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
 int launch_act_tangent(float* hdot, const float* h, const float* beta, long n, hipStream_t s) {
   hipLaunchKernelGGL(act_tangent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdot, h, beta, n);
   INF_CHECK_LAUNCH();

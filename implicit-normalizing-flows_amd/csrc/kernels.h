@@ -191,6 +191,7 @@ int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int launch_act_bwd1(const float* ga, const float* h, const float* beta, float* gprev, double* bpart, long n,
                     int nblocks, hipStream_t s);
 int launch_act_tangent(float* hdot, const float* h, const float* beta, long n, hipStream_t s);
+int launch_swish_apply(const float* h, const float* beta, float* out, long n, hipStream_t s);
 int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, const float* beta,
                     float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks, hipStream_t s);
 int launch_channel_sum(const float* g, int B, int C, int P, float* out, hipStream_t s);
