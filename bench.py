@@ -186,8 +186,9 @@ def main():
                  if mm == 'bf16x6' else 'f32: v_mfma_f32_32x32x2_f32'),
         'data': 'synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
                 % 'x'.join(map(str, arch['input_size'])),
-        'config': {'workload': '%s implicit flow density eval (run_cifar10.sh arch%s), batch %d per GPU'
-                               % (args.config, '' if args.config == 'cifar10' else ' variant', B),
+        'config': {'workload': '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU'
+                               % (args.config, 'density eval' if args.mode == 'eval' else 'training step',
+                                  '' if args.config == 'cifar10' else ' variant', B),
                    'global_batch': B * world, 'per_gpu_batch': B, 'parallelism': 'dp%d' % world,
                    'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps},
         'bits_per_dim': round(bpd, 6),

@@ -708,6 +708,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
 // ---------------------------------------------------------------------------------------------
 struct GradBufs {
   std::vector<float*> H, Hd, Ad;     // pre-activations, their tangents, activation tangents (Ad[0]: input)
+  std::vector<float*> A;             // layer inputs after their swish (A[0] = preact(x)), computed once per call
   float *gA, *gB, *hA, *hB, *gad, *ga, *Y, *slab, *dWe, *dWe2, *dsig, *xin, *tmp_in, *act;
   double *bpart, *dot;
   int max_split;
@@ -727,6 +728,8 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
   for (auto& p : g.H) p = w.take<float>(hid);
   for (auto& p : g.Hd) p = w.take<float>(hid);
   for (int l = 0; l < L; ++l) g.Ad[l] = w.take<float>(l == 0 ? in : hid);
+  g.A.resize(L > 0 ? L : 0);
+  for (int l = 0; l < L; ++l) g.A[l] = w.take<float>(l == 0 ? in : hid);
   for (float** p : {&g.gA, &g.gB, &g.hA, &g.hB, &g.gad, &g.ga}) *p = w.take<float>(std::max(hid, in));
   g.Y = w.take<float>((size_t)B * n->rows_max * n->P);
   g.slab = w.take<float>((size_t)GRAD_SPLIT * mn);
@@ -740,6 +743,21 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
   g.dot = w.take<double>(128);      // [0] the dot, [1..64] its block partials
   g.max_split = GRAD_SPLIT;
   return w.off + 256;
+}
+
+// Input of layer l as the GEMMs consume it: x (l = 0) or H[l-1], with its swish (preact / activation)
+// applied once into gb.A[l] instead of in every output tile's loader.  Returns the operand, no beta left.
+static int layer_input(InfNet* n, int l, const float* x, GradBufs& gb, int B, hipStream_t s, const float** out) {
+  const float* in = l == 0 ? x : gb.H[l - 1];
+  const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+  if (!pb) {
+    *out = in;
+    return INF_OK;
+  }
+  const long ne = (long)B * n->L[l].cin * n->P;
+  INF_TRY(launch_swish_apply(in, pb, gb.A[l], ne, s));
+  *out = gb.A[l];
+  return INF_OK;
 }
 
 // h_l = W_l * in (+ b_l); in gets swish(., pre_beta) on load when pre_beta is set.  l < L-1 (no taps).
@@ -1744,19 +1762,17 @@ int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, 
   if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
   const int L = (int)n->L.size();
   const long hidP = (long)n->P;
-  // forward: pre-activations
-  for (int l = 0; l + 1 < L; ++l) {
-    const float* in = l == 0 ? x : gb.H[l - 1];
-    const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
-    INF_TRY(layer_fwd(n, l, in, pb, true, gb.H[l], B, s));
+  // forward: pre-activations (each layer's input activated once, gb.A)
+  std::vector<const float*> Ain(L, nullptr);
+  for (int l = 0; l < L; ++l) {
+    INF_TRY(layer_input(n, l, x, gb, B, s, &Ain[l]));
+    if (l + 1 < L) INF_TRY(layer_fwd(n, l, Ain[l], nullptr, true, gb.H[l], B, s));
   }
   // backward
   const float* g = gout;
   float* bufs[2] = {gb.gA, gb.gB};
   for (int l = L - 1; l >= 0; --l) {
-    const float* X = l == 0 ? x : gb.H[l - 1];
-    const float* xb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
-    INF_TRY(layer_param_grads(n, l, nullptr, nullptr, g, X, xb, gr, B, gb, s));
+    INF_TRY(layer_param_grads(n, l, nullptr, nullptr, g, Ain[l], nullptr, gr, B, gb, s));
     if (l > 0) {
       const WLayer& prev = n->L[l - 1];
       const long ne = (long)B * prev.cout * hidP;
@@ -1801,10 +1817,10 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
     in_tan = gb.Ad[0];
   }
   // forward: primal pre-activations H, tangents Hd, activation tangents Ad
+  std::vector<const float*> Ain(L, nullptr);     // each layer's input activated once (gb.A)
   for (int l = 0; l + 1 < L; ++l) {
-    const float* in = l == 0 ? x : gb.H[l - 1];
-    const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
-    INF_TRY(layer_fwd(n, l, in, pb, true, gb.H[l], B, s));
+    INF_TRY(layer_input(n, l, x, gb, B, s, &Ain[l]));
+    INF_TRY(layer_fwd(n, l, Ain[l], nullptr, true, gb.H[l], B, s));
     const float* tin = l == 0 ? in_tan : gb.Ad[l];
     INF_TRY(layer_fwd(n, l, tin, nullptr, false, gb.Hd[l], B, s));
     const long ne = (long)B * n->L[l].cout * n->P;
@@ -1818,8 +1834,9 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
   float* pb2[2] = {gb.hA, gb.hB};
   for (int l = L - 1; l >= 0; --l) {
     const float* X_tan = l == 0 ? in_tan : gb.Ad[l];
-    const float* X_pri = l == 0 ? x : gb.H[l - 1];
-    const float* xb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
+    if (!Ain[l]) INF_TRY(layer_input(n, l, x, gb, B, s, &Ain[l]));   // (the last layer's input)
+    const float* X_pri = Ain[l];
+    const float* xb = nullptr;
     INF_TRY(layer_param_grads(n, l, G_tan, X_tan, G_pri, X_pri, xb, gr, B, gb, s));
     INF_TRY(layer_vjp(n, l, G_tan, gb.gad, B, gb, s));
     if (G_pri) INF_TRY(layer_vjp(n, l, G_pri, gb.ga, B, gb, s));
