@@ -1024,8 +1024,8 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       n->mfma_mode = (mm && mm[0] == 'f') ? INF_MFMA_F32 : INF_MFMA_BF16X6;
     }
   }
-  // sigma scratch: one partial per 256 output elements of the largest conv
-  size_t sc = 64;
+  // sigma scratch: one partial per 256 output elements of the largest conv (or per channel-split block)
+  size_t sc = SIGMA_MAX_PARTS + 64;
   for (auto& w : n->L) sc = std::max(sc, (size_t)w.cout * (n->fc ? 1 : n->P) / 256 + 64);
   n->scratch_doubles = sc;
   if (hipGetDevice(&n->device) != hipSuccess) n->device = 0;

@@ -95,6 +95,7 @@ struct BroydenArgs {
 int launch_broyden_update(const BroydenArgs& a, hipStream_t s);
 
 // Spectral scale: sigma = u . (W v) for conv (pad k//2) or matrix; factor = max(1, sigma / coeff)
+constexpr int SIGMA_MAX_PARTS = 4096;   // launch_sigma's partial count bound when it splits channels
 int launch_sigma(const float* W, const float* u, const float* v, int cout, int cin, int ks, int H, int Wd,
                  float coeff, float* factor_out, float* scratch, hipStream_t s);
 // Packed operand:  dst[(mrow)][kcol] built from W / factor with the given pack mode.

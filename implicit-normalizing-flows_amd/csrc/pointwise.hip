@@ -491,20 +491,23 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 // spectral normalisation (mixed_lipschitz.py:126-132, 320-326, 378-386) and operand packing
 // ------------------------------------------------------------------------------------------
-// sigma partials: one thread per output element (o, y, x): (W v)[o,y,x] * u[o,y,x]
+// sigma partials: one thread per output element (o, y, x) and input-channel chunk (blockIdx.y):
+// sum_c (W v)[o,y,x] * u[o,y,x].  Splitting the channel sum over the grid keeps the small-cout layers
+// (the 512 -> C output conv: cout*H*W = 3072 elements, 4608 MACs each) from running as 12 serial blocks.
 __global__ __launch_bounds__(256) void sigma_partial_kernel(const float* W, const float* u, const float* v, int cout,
-                                                            int cin, int ks, int H, int Wd, double* part) {
+                                                            int cin, int ks, int H, int Wd, int cchunk, double* part) {
   __shared__ double red[16];
   const int P = H * Wd;
   const long n = (long)cout * P;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = blockIdx.y * cchunk, c1 = min(cin, c0 + cchunk);
   double val = 0.0;
   if (i < n) {
     const int o = i / P, p = i - (long)o * P;
     const int y = p / Wd, x = p - y * Wd;
     const int pad = ks / 2;
     float s = 0.f;
-    for (int c = 0; c < cin; ++c)
+    for (int c = c0; c < c1; ++c)
       for (int dy = 0; dy < ks; ++dy)
         for (int dx = 0; dx < ks; ++dx) {
           const int yy = y + dy - pad, xx = x + dx - pad;
@@ -514,12 +517,14 @@ __global__ __launch_bounds__(256) void sigma_partial_kernel(const float* W, cons
     val = (double)s * (double)u[i];
   }
   val = block_sum(val, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = val;
+  if (threadIdx.x == 0) part[(long)blockIdx.y * gridDim.x + blockIdx.x] = val;
 }
-__global__ void sigma_final_kernel(const double* part, int nparts, float coeff, float* factor) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void sigma_final_kernel(const double* part, int nparts, float coeff, float* factor) {
+  __shared__ double red[16];
   double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += part[i];
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
+  s = block_sum(s, red);
+  if (threadIdx.x != 0) return;
   const float sigma = (float)s;
   const float r = sigma / coeff;
   factor[0] = r > 1.f ? r : 1.f;    // torch.max(ones(1), sigma / coeff)
@@ -529,10 +534,16 @@ int launch_sigma(const float* W, const float* u, const float* v, int cout, int c
                  float coeff, float* factor_out, float* scratch, hipStream_t s) {
   const long n = (long)cout * H * Wd;
   const int nb = (int)((n + 255) / 256);
+  // channel chunks so that ~2048 blocks run; never more than SIGMA_MAX_PARTS partials (scratch size)
+  int csplit = 1;
+  if (nb < 2048 && cin > 1) csplit = std::min<long>(cin, std::max<long>(1, std::min<long>(2048, SIGMA_MAX_PARTS) / nb));
+  const int cchunk = (cin + csplit - 1) / csplit;
+  csplit = (cin + cchunk - 1) / cchunk;
   double* part = reinterpret_cast<double*>(scratch);
-  hipLaunchKernelGGL(sigma_partial_kernel, dim3(nb), dim3(256), 0, s, W, u, v, cout, cin, ks, H, Wd, part);
+  hipLaunchKernelGGL(sigma_partial_kernel, dim3(nb, csplit), dim3(256), 0, s, W, u, v, cout, cin, ks, H, Wd, cchunk,
+                     part);
   INF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sigma_final_kernel, dim3(1), dim3(64), 0, s, part, nb, coeff, factor_out);
+  hipLaunchKernelGGL(sigma_final_kernel, dim3(1), dim3(256), 0, s, part, nb * csplit, coeff, factor_out);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

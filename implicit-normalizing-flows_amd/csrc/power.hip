@@ -72,6 +72,66 @@ __global__ void pi_apply_wt(PIOp op, const float* __restrict__ y, float* __restr
   x[i] = acc;
 }
 
+// Few-output variants (fewer than PI_WAVE_MAX outputs, e.g. the 512 -> 3 conv's W v: 3072 outputs of
+// 4608 terms): one wave per output element, the lanes split the reduction (fixed order), wave sum.
+constexpr long PI_WAVE_MAX = 65536;
+__global__ __launch_bounds__(256) void pi_apply_w_wave(PIOp op, const float* __restrict__ x, float* __restrict__ y,
+                                                       const PIState* st) {
+  if (st && st->done) return;
+  const int P = op.H * op.Wd;
+  const long n = (long)op.cout * P;
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;                               // wave-uniform
+  const int o = (int)(i / P), p = (int)(i - (long)o * P);
+  const int py = p / op.Wd, px = p - py * op.Wd;
+  const int ks = op.ks, r = ks / 2, kk = ks * ks;
+  const float* w = op.W + (long)o * op.cin * kk;
+  float acc = 0.f;
+  for (int j = lane; j < op.cin * kk; j += 64) {
+    const int c = j / kk, t = j - c * kk;
+    const int yy = py + t / ks - r, xx = px + t % ks - r;
+    if (yy >= 0 && yy < op.H && xx >= 0 && xx < op.Wd) acc = fmaf(w[j], x[(long)c * P + yy * op.Wd + xx], acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) y[i] = acc;
+}
+__global__ __launch_bounds__(256) void pi_apply_wt_wave(PIOp op, const float* __restrict__ y, float* __restrict__ x,
+                                                        const PIState* st) {
+  if (st && st->done) return;
+  const int P = op.H * op.Wd;
+  const long n = (long)op.cin * P;
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const int c = (int)(i / P), q = (int)(i - (long)c * P);
+  const int qy = q / op.Wd, qx = q - qy * op.Wd;
+  const int ks = op.ks, r = ks / 2, kk = ks * ks;
+  float acc = 0.f;
+  for (int j = lane; j < op.cout * kk; j += 64) {
+    const int o = j / kk, t = j - o * kk;
+    const int yy = qy - t / ks + r, xx = qx - t % ks + r;
+    if (yy >= 0 && yy < op.H && xx >= 0 && xx < op.Wd)
+      acc = fmaf(op.W[((long)o * op.cin + c) * kk + t], y[(long)o * P + yy * op.Wd + xx], acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) x[i] = acc;
+}
+static void pi_launch_w(const PIOp& op, const float* x, float* y, const PIState* st, hipStream_t s) {
+  const long n = (long)op.cout * op.H * op.Wd;
+  if (n < PI_WAVE_MAX)
+    hipLaunchKernelGGL(pi_apply_w_wave, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, op, x, y, st);
+  else
+    hipLaunchKernelGGL(pi_apply_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, op, x, y, st);
+}
+static void pi_launch_wt(const PIOp& op, const float* y, float* x, const PIState* st, hipStream_t s) {
+  const long n = (long)op.cin * op.H * op.Wd;
+  if (n < PI_WAVE_MAX)
+    hipLaunchKernelGGL(pi_apply_wt_wave, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, op, y, x, st);
+  else
+    hipLaunchKernelGGL(pi_apply_wt, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, op, y, x, st);
+}
+
 __device__ double block_reduce_sum(double v, double* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -126,6 +186,89 @@ __global__ __launch_bounds__(1024) void pi_normalize(const float* __restrict__ s
     const double tol_v = (double)st->atol + (double)st->rtol * mx;
     if (st->err_u < tol_u && err < tol_v) st->done = 1;
   }
+}
+
+// Long vectors (a k x k conv's u or v: cout*H*W up to 512K) use PI_NB workgroups instead of one:
+//   pi_dot_part   partial sums of a.b per workgroup (grid-stride, fixed order)
+//   pi_norm_apply every workgroup re-reduces the partials (same order, same result), normalises its
+//                 slice in place and writes partial |new - old|^2 and max
+//   pi_norm_final one workgroup: err / max / convergence as pi_normalize
+constexpr int PI_NB = 256;
+constexpr long PI_MULTI_MIN = 16384;
+__global__ __launch_bounds__(256) void pi_dot_part(const float* __restrict__ a, const float* __restrict__ b, long n,
+                                                   const PIState* st, double* part) {
+  __shared__ double red[16];
+  if (st && st->done) return;
+  double acc = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    acc += (double)a[i] * (double)b[i];
+  acc = block_reduce_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void pi_norm_apply(const float* __restrict__ s, float* vec, long n,
+                                                     const PIState* st, const double* part, double* part_e,
+                                                     double* part_m) {
+  __shared__ double red[16];
+  if (st->done) return;
+  double ss = threadIdx.x < gridDim.x ? part[threadIdx.x] : 0.0;
+  ss = block_reduce_sum(ss, red);
+  const float nrm = fmaxf((float)sqrt(ss), 1e-12f);
+  double e = 0.0, mx = -INFINITY;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float nv = s[i] / nrm;
+    const double d = (double)nv - (double)vec[i];
+    e += d * d;
+    mx = fmax(mx, (double)nv);
+    vec[i] = nv;
+  }
+  e = block_reduce_sum(e, red);
+  mx = block_reduce_max(mx, red);
+  if (threadIdx.x == 0) {
+    part_e[blockIdx.x] = e;
+    part_m[blockIdx.x] = mx;
+  }
+}
+__global__ __launch_bounds__(256) void pi_norm_final(long n, int nparts, PIState* st, const double* part_e,
+                                                     const double* part_m, int which) {
+  __shared__ double red[16];
+  if (st->done) return;
+  double e = threadIdx.x < nparts ? part_e[threadIdx.x] : 0.0;
+  double mx = threadIdx.x < nparts ? part_m[threadIdx.x] : -INFINITY;
+  e = block_reduce_sum(e, red);
+  mx = block_reduce_max(mx, red);
+  if (threadIdx.x != 0) return;
+  const double err = sqrt(e) / sqrt((double)n);
+  if (which == 0) {
+    st->err_u = err;
+    st->max_u = mx;
+    return;
+  }
+  st->iters += 1;
+  if (st->use_tol) {
+    const double tol_u = (double)st->atol + (double)st->rtol * st->max_u;
+    const double tol_v = (double)st->atol + (double)st->rtol * mx;
+    if (st->err_u < tol_u && err < tol_v) st->done = 1;
+  }
+}
+__global__ __launch_bounds__(256) void pi_sigma_final(const double* part, int nparts, PIState* st, float* scale) {
+  __shared__ double red[16];
+  double v = threadIdx.x < nparts ? part[threadIdx.x] : 0.0;
+  v = block_reduce_sum(v, red);
+  if (threadIdx.x == 0) {
+    st->sigma = v;
+    if (scale) *scale = (float)v;
+  }
+}
+// scratch: 3 * PI_NB doubles
+static void pi_launch_normalize(const float* sv, float* vec, long n, PIState* st, int which, double* scr,
+                                hipStream_t s) {
+  if (n < PI_MULTI_MIN) {
+    hipLaunchKernelGGL(pi_normalize, dim3(1), dim3(1024), 0, s, sv, vec, n, st, which);
+    return;
+  }
+  hipLaunchKernelGGL(pi_dot_part, dim3(PI_NB), dim3(256), 0, s, sv, sv, n, st, scr);
+  hipLaunchKernelGGL(pi_norm_apply, dim3(PI_NB), dim3(256), 0, s, sv, vec, n, st, scr, scr + PI_NB, scr + 2 * PI_NB);
+  hipLaunchKernelGGL(pi_norm_final, dim3(1), dim3(256), 0, s, n, PI_NB, st, scr + PI_NB, scr + 2 * PI_NB, which);
 }
 
 __global__ void pi_init(PIState* st, int use_tol, float atol, float rtol) {
@@ -186,7 +329,7 @@ extern "C" {
 size_t inf_power_iteration_workspace_bytes(const InfPowerIterDesc* d) {
   if (!pi_valid(d)) return 0;
   const PIOp op = pi_op(d);
-  return 256 + (size_t)(pi_nu(op) + pi_nv(op)) * sizeof(float) + 256;
+  return 256 + (size_t)(pi_nu(op) + pi_nv(op)) * sizeof(float) + 256 + 3 * PI_NB * sizeof(double);
 }
 
 int inf_power_iteration(const InfPowerIterDesc* d, int max_iters, int use_tol, float atol, float rtol,
@@ -200,36 +343,41 @@ int inf_power_iteration(const InfPowerIterDesc* d, int max_iters, int use_tol, f
   PIState* st = reinterpret_cast<PIState*>(base);
   float* us = reinterpret_cast<float*>(base + 256);
   float* vs = us + nu;
+  double* scr = reinterpret_cast<double*>(base + 256 + (((size_t)(nu + nv) * sizeof(float) + 255) / 256) * 256);
   PIState h;
   memset(&h, 0, sizeof(h));
   hipLaunchKernelGGL(pi_init, dim3(1), dim3(1), 0, s, st, use_tol ? 1 : 0, atol, rtol);
-  const dim3 gu((unsigned)((nu + 255) / 256)), gv((unsigned)((nv + 255) / 256));
-  constexpr int CHUNK = 8;
-  int done_iters = 0;
+  // speculative chunks of 2, 4, 8, 8, ... iterations between flag reads (a nearly converged u, v, as
+  // after one optimiser step, stops within the first chunk)
+  int done_iters = 0, chunk = use_tol ? 2 : max_iters;
   while (done_iters < max_iters) {
-    const int n = std::min(CHUNK, max_iters - done_iters);
+    const int n = std::min(chunk, max_iters - done_iters);
     for (int k = 0; k < n; ++k) {
-      hipLaunchKernelGGL(pi_apply_w, gu, dim3(256), 0, s, op, d->v, us, st);
-      hipLaunchKernelGGL(pi_normalize, dim3(1), dim3(1024), 0, s, us, d->u, nu, st, 0);
-      hipLaunchKernelGGL(pi_apply_wt, gv, dim3(256), 0, s, op, d->u, vs, st);
-      hipLaunchKernelGGL(pi_normalize, dim3(1), dim3(1024), 0, s, vs, d->v, nv, st, 1);
+      pi_launch_w(op, d->v, us, st, s);
+      pi_launch_normalize(us, d->u, nu, st, 0, scr, s);
+      pi_launch_wt(op, d->u, vs, st, s);
+      pi_launch_normalize(vs, d->v, nv, st, 1, scr, s);
     }
     INF_CHECK_LAUNCH();
     done_iters += n;
+    chunk = std::min(2 * chunk, 8);
     if (!use_tol) continue;
     INF_HIP(hipMemcpyAsync(&h, st, sizeof(h), hipMemcpyDeviceToHost, s));
     INF_HIP(hipStreamSynchronize(s));
     if (h.done) break;
   }
   // sigma = u . (W v)   (mixed_lipschitz.py:126,317,378-380)
-  hipLaunchKernelGGL(pi_apply_w, gu, dim3(256), 0, s, op, d->v, us, nullptr);
-  hipLaunchKernelGGL(pi_sigma, dim3(1), dim3(1024), 0, s, d->u, us, nu, st, d->scale);
-  INF_CHECK_LAUNCH();
-  if (iters_used) {
-    INF_HIP(hipMemcpyAsync(&h, st, sizeof(h), hipMemcpyDeviceToHost, s));
-    INF_HIP(hipStreamSynchronize(s));
-    *iters_used = h.iters;
+  pi_launch_w(op, d->v, us, nullptr, s);
+  if (nu < PI_MULTI_MIN) {
+    hipLaunchKernelGGL(pi_sigma, dim3(1), dim3(1024), 0, s, d->u, us, nu, st, d->scale);
+  } else {
+    hipLaunchKernelGGL(pi_dot_part, dim3(PI_NB), dim3(256), 0, s, d->u, us, nu, nullptr, scr);
+    hipLaunchKernelGGL(pi_sigma_final, dim3(1), dim3(256), 0, s, scr, PI_NB, st, d->scale);
   }
+  INF_CHECK_LAUNCH();
+  // the count needs no further readback: with the tolerance test the last flag read came after every
+  // iteration kernel; without it every iteration runs
+  if (iters_used) *iters_used = use_tol ? h.iters : max_iters;
   return INF_OK;
 }
 
