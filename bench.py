@@ -64,6 +64,9 @@ def parse():
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
     ap.add_argument('--cpu-batch', type=int, default=16, help='images in the bounded CPU-baseline sample (~10-15 s)')
+    ap.add_argument('--train-step', default='full', choices=['full', 'fwdbwd'],
+                    help='train mode: full = forward + backward + clip_grad_norm_(1) + Adam + update_lipschitz + '
+                         'EMA (train_img.py:637-658); fwdbwd = forward + backward only')
     ap.add_argument('--mode', default='eval', choices=['eval', 'train'],
                     help='eval: the density-evaluation hot path (BASELINE metric); train: one training step '
                          '(train-mode forward + loss.backward(), train_img.py:611-638; no optimizer step)')
@@ -117,6 +120,10 @@ def main():
     if args.mode == 'train':
         model.train()                          # probes: --probes (device RNG by default, as in eval)
         params = [p for p in model.parameters() if p.requires_grad]
+        if args.train_step == 'full':          # train_img.py:465 (Adam, betas 0.9 / 0.99), :653-658, utils.py:126
+            from lib.utils import ExponentialMovingAverage, update_lipschitz
+            opt = torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.99), weight_decay=0)
+            ema = ExponentialMovingAverage(model, decay=0.999)
 
     def step(i):
         if args.mode == 'train':
@@ -126,6 +133,12 @@ def main():
             bpd.backward()
             if world > 1:                      # data-parallel gradient all-reduce (one flat bucket)
                 dd.allreduce_grads(params)
+            if args.train_step == 'full':
+                torch.nn.utils.clip_grad_norm_(params, 1.)
+                opt.step()
+                opt.zero_grad()
+                update_lipschitz(model)
+                ema.apply()
             return bpd.detach()
         _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
         s, n = dd.global_logpx_sum(logpx)      # the one collective per batch
@@ -177,7 +190,9 @@ def main():
     peak = X6_PEAK_TFLOPS if (mm == 'bf16x6' and fused_dom) else FP32_MFMA_PEAK_TFLOPS
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
-        'samples/sec (whole node), %s training step (forward + backward)' % args.config,
+        'samples/sec (whole node), %s training step (%s)' % (
+            args.config, 'forward + backward + grad clip + Adam + update_lipschitz + EMA'
+            if args.train_step == 'full' else 'forward + backward'),
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',

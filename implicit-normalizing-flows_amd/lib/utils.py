@@ -10,7 +10,7 @@ import os
 
 import torch
 
-__all__ = ['ExponentialMovingAverage', 'save_checkpoint', 'load_checkpoint']
+__all__ = ['ExponentialMovingAverage', 'update_lipschitz', 'save_checkpoint', 'load_checkpoint']
 
 
 class ExponentialMovingAverage(object):
@@ -30,9 +30,12 @@ class ExponentialMovingAverage(object):
         if len(self.shadow_params) == 0:
             self.init()
         else:
-            with torch.no_grad():
-                for name, param in self.module.named_parameters():
-                    self.shadow_params[name] -= (1 - self.decay) * (self.shadow_params[name] - param.data)
+            with torch.no_grad():         # the reference's per-parameter update, as grouped kernels
+                names, params = zip(*[(n, p.data) for n, p in self.module.named_parameters()])
+                shadows = [self.shadow_params[n] for n in names]
+                diff = torch._foreach_sub(shadows, list(params))
+                torch._foreach_mul_(diff, 1 - self.decay)
+                torch._foreach_sub_(shadows, diff)
 
     def set(self, other_ema):
         self.init()
@@ -61,6 +64,26 @@ class ExponentialMovingAverage(object):
     def __repr__(self):
         return '{}(decay={}, module={}, nparams={})'.format(self.__class__.__name__, self.decay,
                                                             self.module.__class__.__name__, self.nparams)
+
+
+def update_lipschitz(model):
+    """compute_weight(update=True) on every InducedNorm conv / linear of `model` (train_img.py:786-792),
+    run after each optimiser step; on CUDA each call is one engine power iteration (power.hip).
+
+    The imBlocks' frozen copies (nnet_x_copy / nnet_z_copy) are skipped: the next forward overwrites
+    every one of their parameters and buffers from nnet_x / nnet_z (implicit_block.py:228-229), so
+    updating them, as the reference's walk over model.modules() does, has no observable effect."""
+    from .layers.base import InducedNormConv2d, InducedNormLinear
+    skip = set()
+    for m in model.modules():
+        for name in ('nnet_x_copy', 'nnet_z_copy'):
+            cp = getattr(m, name, None)
+            if isinstance(cp, torch.nn.Module):
+                skip.update(id(c) for c in cp.modules())
+    with torch.no_grad():
+        for m in model.modules():
+            if id(m) not in skip and isinstance(m, (InducedNormConv2d, InducedNormLinear)):
+                m.compute_weight(update=True)
 
 
 def save_checkpoint(path, model, ema=None, **extra):
