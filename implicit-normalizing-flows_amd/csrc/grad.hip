@@ -261,6 +261,69 @@ __global__ __launch_bounds__(256) void wgrad_valu_kernel(WgradArgs a) {
     if (m < a.M) out[(long)m * a.N + n] = acc[m];
 }
 
+// 3x3 form of the small-M kernel: one thread per (input channel, tap row dy) keeps the three dx taps of
+// all M outputs in registers, so one row segment of X (two dwordx4 + two halo dwords per 8 pixels) feeds
+// 3 taps instead of 1.  Same per-element summation order as wgrad_valu_kernel.
+__global__ __launch_bounds__(256) void wgrad_valu3_kernel(WgradArgs a) {
+  const int n3 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int split = blockIdx.y;
+  const long rows = (long)a.B * a.H;
+  const long r_lo = (rows * split) / a.nsplit, r_hi = (rows * (split + 1)) / a.nsplit;
+  const float bs = a.x_beta ? softplus_f(*a.x_beta) : 0.f;
+  const int cin = a.N / 9;
+  const bool valid = n3 < cin * 3;
+  const int i = valid ? n3 / 3 : 0, dyi = valid ? n3 - 3 * i : 0;
+  float acc[WGV_MAXM][3];
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m) acc[m][0] = acc[m][1] = acc[m][2] = 0.f;
+  for (long row = r_lo; row < r_hi; ++row) {
+    const long b = row / a.H;
+    const int y = (int)(row - b * a.H);
+    const int yy = y + dyi - 1;
+    const bool yin = valid && yy >= 0 && yy < a.H;
+    const float* xr = a.X + b * a.x_sample + (long)i * a.P + (long)yy * a.W;
+    const float* gr = a.G + b * a.g_sample + (long)y * a.W;
+    for (int x0 = 0; x0 < a.W; x0 += 8) {
+      float xv[10];                                   // X[x0 - 1 .. x0 + 8] of this row, 0 outside
+      if (yin) {
+        const float4 c0 = *reinterpret_cast<const float4*>(xr + x0);
+        const float4 c1 = *reinterpret_cast<const float4*>(xr + x0 + 4);
+        xv[1] = c0.x; xv[2] = c0.y; xv[3] = c0.z; xv[4] = c0.w;
+        xv[5] = c1.x; xv[6] = c1.y; xv[7] = c1.z; xv[8] = c1.w;
+        xv[0] = x0 > 0 ? xr[x0 - 1] : 0.f;
+        xv[9] = x0 + 8 < a.W ? xr[x0 + 8] : 0.f;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 10; ++u) xv[u] = 0.f;
+      }
+      if (a.x_beta) {
+#pragma unroll
+        for (int u = 0; u < 10; ++u) xv[u] = swish_f(xv[u], bs);
+      }
+#pragma unroll
+      for (int m = 0; m < WGV_MAXM; ++m)
+        if (m < a.M) {
+          const float4 g0 = *reinterpret_cast<const float4*>(gr + (long)m * a.P + x0);
+          const float4 g1 = *reinterpret_cast<const float4*>(gr + (long)m * a.P + x0 + 4);
+          const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[m][dx] = fmaf(g[u], xv[u + dx], acc[m][dx]);
+        }
+    }
+  }
+  if (!valid) return;
+  float* out = a.slab + (long)split * a.M * a.N + (long)i * 9 + dyi * 3;
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m)
+    if (m < a.M) {
+      out[(long)m * a.N] = acc[m][0];
+      out[(long)m * a.N + 1] = acc[m][1];
+      out[(long)m * a.N + 2] = acc[m][2];
+    }
+}
+
 // out[i] = sum_s slab[s][i] (fp64, fixed order) (* scale)
 __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float* out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,17 +333,30 @@ __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float*
   out[i] = (float)s;
 }
 
+static bool wgrad_valu3_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("INFLOW_WGRAD_VALU3");               // debug knob: 0 = one-tap kernel
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0) {
-    const int nb = (a.N + 255) / 256;
+    const bool three = a.ks == 3 && a.x_sample % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0 &&
+                       wgrad_valu3_enabled();
+    const int nb = three ? (a.N / 3 + 255) / 256 : (a.N + 255) / 256;
     const long rows = (long)a.B * a.H;
     int nsplit = (int)std::max<long>(1, std::min<long>(rows, 2048 / std::max(1, nb)));
     if (nsplit > a.max_split) nsplit = a.max_split;
     a.nsplit = nsplit;
     const bool prof = prof_enabled();
     if (prof) prof_begin_launch(s);
-    hipLaunchKernelGGL(wgrad_valu_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
+    if (three)
+      hipLaunchKernelGGL(wgrad_valu3_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(wgrad_valu_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
     INF_CHECK_LAUNCH();
     if (prof) {
       const double K = (double)a.B * a.P;
