@@ -221,7 +221,7 @@ def main():
                                      'ms': round(s['total_ms'], 3),
                                      'tflops': round(s['flops'] / (s['total_ms'] * 1e9), 2) if s['flops'] else None,
                                      'gbs': round(s['bytes'] / (s['total_ms'] * 1e6), 1)}
-                                    for s in stats], key=lambda r: -r['ms'])[:8]},
+                                    for s in stats], key=lambda r: -r['ms'])[:12]},
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline and args.config != 'celebahq256' and args.mode == 'eval':

@@ -324,6 +324,81 @@ __global__ __launch_bounds__(256) void wgrad_valu3_kernel(WgradArgs a) {
     }
 }
 
+// Row-resident form of wgrad_valu3_kernel for W in {8, 16, 32}: the whole X row segment (W + 2 halo) sits in
+// registers and the next row's is loaded before the current row is consumed, so a wave has one HBM round
+// trip in flight per row instead of one dependent load per 8 pixels (the one-chunk kernel was latency-bound:
+// 8 waves per SIMD, each a chain of ~24 serial misses).  Per accumulator the additions still run over x
+// ascending within a row and rows ascending, i.e. the same order as wgrad_valu3_kernel.
+template <int WW>
+__global__ __launch_bounds__(256) void wgrad_valu3r_kernel(WgradArgs a) {
+  const int n3 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int split = blockIdx.y;
+  const long rows = (long)a.B * a.H;
+  const long r_lo = (rows * split) / a.nsplit, r_hi = (rows * (split + 1)) / a.nsplit;
+  const float bs = a.x_beta ? softplus_f(*a.x_beta) : 0.f;
+  const int cin = a.N / 9;
+  const bool valid = n3 < cin * 3;
+  const int i = valid ? n3 / 3 : 0, dyi = valid ? n3 - 3 * i : 0;
+  float acc[WGV_MAXM][3];
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m) acc[m][0] = acc[m][1] = acc[m][2] = 0.f;
+  auto load_row = [&](long row, float* xv) {          // xv[0] = X[-1], xv[1..WW] = X[0..WW-1], xv[WW+1] = X[WW]
+    const long b = row / a.H;
+    const int y = (int)(row - b * a.H);
+    const int yy = y + dyi - 1;
+    if (valid && yy >= 0 && yy < a.H) {
+      const float* xr = a.X + b * a.x_sample + (long)i * a.P + (long)yy * WW;
+#pragma unroll
+      for (int q = 0; q < WW / 4; ++q) {
+        const float4 c = *reinterpret_cast<const float4*>(xr + 4 * q);
+        xv[1 + 4 * q] = c.x; xv[2 + 4 * q] = c.y; xv[3 + 4 * q] = c.z; xv[4 + 4 * q] = c.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 1; u <= WW; ++u) xv[u] = 0.f;
+    }
+    xv[0] = 0.f;
+    xv[WW + 1] = 0.f;
+  };
+  float cur[WW + 2], nxt[WW + 2];
+  if (r_lo < r_hi) load_row(r_lo, cur);
+  for (long row = r_lo; row < r_hi; ++row) {
+    if (row + 1 < r_hi) load_row(row + 1, nxt);
+    if (a.x_beta) {
+#pragma unroll
+      for (int u = 1; u <= WW; ++u) cur[u] = swish_f(cur[u], bs);
+    }
+    const long b = row / a.H;
+    const int y = (int)(row - b * a.H);
+    const float* gr = a.G + b * a.g_sample + (long)y * WW;
+#pragma unroll
+    for (int m = 0; m < WGV_MAXM; ++m)
+      if (m < a.M) {
+        float g[WW];
+#pragma unroll
+        for (int q = 0; q < WW / 4; ++q) {
+          const float4 c = *reinterpret_cast<const float4*>(gr + (long)m * a.P + 4 * q);
+          g[4 * q] = c.x; g[4 * q + 1] = c.y; g[4 * q + 2] = c.z; g[4 * q + 3] = c.w;
+        }
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int u = 0; u < WW; ++u) acc[m][dx] = fmaf(g[u], cur[u + dx], acc[m][dx]);
+      }
+#pragma unroll
+    for (int u = 0; u < WW + 2; ++u) cur[u] = nxt[u];
+  }
+  if (!valid) return;
+  float* out = a.slab + (long)split * a.M * a.N + (long)i * 9 + dyi * 3;
+#pragma unroll
+  for (int m = 0; m < WGV_MAXM; ++m)
+    if (m < a.M) {
+      out[(long)m * a.N] = acc[m][0];
+      out[(long)m * a.N + 1] = acc[m][1];
+      out[(long)m * a.N + 2] = acc[m][2];
+    }
+}
+
 // out[i] = sum_s slab[s][i] (fp64, fixed order) (* scale)
 __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float* out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,6 +416,14 @@ static bool wgrad_valu3_enabled() {
   return on;
 }
 
+static bool wgrad_valu3r_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("INFLOW_WGRAD_VALU3R");              // debug knob: 0 = chunked 3-tap kernel
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0) {
@@ -348,12 +431,25 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
                        wgrad_valu3_enabled();
     const int nb = three ? (a.N / 3 + 255) / 256 : (a.N + 255) / 256;
     const long rows = (long)a.B * a.H;
-    int nsplit = (int)std::max<long>(1, std::min<long>(rows, 2048 / std::max(1, nb)));
+    // the row-resident kernel pipelines rows within a wave, so it wants one resident round of waves
+    // (256 CUs x 4 SIMDs x 3 waves at its 145 VGPRs = 768 workgroups) with more rows each
+    const bool resident = three && wgrad_valu3r_enabled() && (a.W == 32 || a.W == 16 || a.W == 8);
+    static const int wg_target = [] {
+      const char* e = getenv("INFLOW_WGRAD_VALU3R_WGS");          // tuning knob
+      return e ? std::max(1, atoi(e)) : 768;
+    }();
+    int nsplit = (int)std::max<long>(1, std::min<long>(rows, (resident ? wg_target : 2048) / std::max(1, nb)));
     if (nsplit > a.max_split) nsplit = a.max_split;
     a.nsplit = nsplit;
     const bool prof = prof_enabled();
     if (prof) prof_begin_launch(s);
-    if (three)
+    if (three && wgrad_valu3r_enabled() && a.W == 32)
+      hipLaunchKernelGGL(wgrad_valu3r_kernel<32>, dim3(nb, nsplit), dim3(256), 0, s, a);
+    else if (three && wgrad_valu3r_enabled() && a.W == 16)
+      hipLaunchKernelGGL(wgrad_valu3r_kernel<16>, dim3(nb, nsplit), dim3(256), 0, s, a);
+    else if (three && wgrad_valu3r_enabled() && a.W == 8)
+      hipLaunchKernelGGL(wgrad_valu3r_kernel<8>, dim3(nb, nsplit), dim3(256), 0, s, a);
+    else if (three)
       hipLaunchKernelGGL(wgrad_valu3_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(wgrad_valu_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
