@@ -470,7 +470,11 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
     const int bm = 64 * tmw, bn = 64 * tnw;
     const int mt = (a.M + bm - 1) / bm, nt = (a.N + bn - 1) / bn;
     const long nchunks = (long)a.B * a.P / WG_K;
-    int nsplit = (int)std::max<long>(1, std::min<long>(nchunks / 4, 1024 / std::max(1, mt * nt)));
+    static const int tiled_wgs = [] {
+      const char* e = getenv("INFLOW_WGRAD_TILED_WGS");           // tuning knob
+      return e ? std::max(1, atoi(e)) : 1024;
+    }();
+    int nsplit = (int)std::max<long>(1, std::min<long>(nchunks / 4, tiled_wgs / std::max(1, mt * nt)));
     if (nsplit > a.max_split) nsplit = a.max_split;
     a.nsplit = nsplit;
     const dim3 grid(mt, nt, nsplit);
