@@ -115,24 +115,18 @@ __global__ __launch_bounds__(256) void wgrad_tiled_kernel(WgradArgs a) {
   const long c_lo = (nchunks * split) / a.nsplit, c_hi = (nchunks * (split + 1)) / a.nsplit;
   const float bs = a.x_beta ? softplus_f(*a.x_beta) : 0.f;
   const int kk9 = a.ks * a.ks, r = a.ks / 2;
-  // fixed (row, pixel-in-chunk) assignment: element j of thread tid is row (tid + 256 j) / 32
-  int grow[GPT], xrow[XPT], gkk[GPT], xkk[XPT], xi[XPT], xdy[XPT], xdx[XPT];
-#pragma unroll
-  for (int j = 0; j < GPT; ++j) {
-    const int e = tid + 256 * j;
-    grow[j] = e / WG_K;
-    gkk[j] = e % WG_K;
-  }
+  // fixed (row, pixel-in-chunk) assignment: element j of thread tid is row (tid + 256 j) / 32 = tid / 32 + 8 j,
+  // pixel tid % 32 (WG_K == 32); per X row only the input channel and the packed tap offset are kept
+  // (fewer live VGPRs -> more resident waves to cover the barriers and operand stores)
+  static_assert(WG_K == 32, "row/pixel assignment assumes 32-pixel chunks");
+  const int kk = tid & 31, rbase = tid >> 5;
+  int xi[XPT], xtap[XPT];
 #pragma unroll
   for (int j = 0; j < XPT; ++j) {
-    const int e = tid + 256 * j;
-    xrow[j] = e / WG_K;
-    xkk[j] = e % WG_K;
-    const int n = n0 + xrow[j];
+    const int n = n0 + rbase + 8 * j;
     const int i = n / kk9, t = n - i * kk9;
     xi[j] = n < a.N ? i : -1;
-    xdy[j] = t / a.ks - r;
-    xdx[j] = t % a.ks - r;
+    xtap[j] = ((t / a.ks - r + 8) << 4) | (t % a.ks - r + 8);
   }
   float gv[GPT], xv[XPT];
   auto load = [&](long c) {
@@ -143,16 +137,16 @@ __global__ __launch_bounds__(256) void wgrad_tiled_kernel(WgradArgs a) {
     const float* Xb = a.X + b * a.x_sample;
 #pragma unroll
     for (int j = 0; j < GPT; ++j) {
-      const int m = m0 + grow[j];
-      gv[j] = m < a.M ? Gb[(long)m * a.P + p0 + gkk[j]] : 0.f;
+      const int m = m0 + rbase + 8 * j;
+      gv[j] = m < a.M ? Gb[(long)m * a.P + p0 + kk] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < XPT; ++j) {
       float v = 0.f;
       if (xi[j] >= 0) {
-        const int p = p0 + xkk[j];
+        const int p = p0 + kk;
         const int py = p / a.W, px = p - py * a.W;
-        const int yy = py + xdy[j], xx = px + xdx[j];
+        const int yy = py + (xtap[j] >> 4) - 8, xx = px + (xtap[j] & 15) - 8;
         if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
           v = Xb[(long)xi[j] * a.P + yy * a.W + xx];
           if (a.x_beta) v = swish_f(v, bs);
@@ -174,9 +168,9 @@ __global__ __launch_bounds__(256) void wgrad_tiled_kernel(WgradArgs a) {
   for (long c = c_lo; c < c_hi; ++c) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < GPT; ++j) Gs[grow[j]][gkk[j]] = gv[j];
+    for (int j = 0; j < GPT; ++j) Gs[rbase + 8 * j][kk] = gv[j];
 #pragma unroll
-    for (int j = 0; j < XPT; ++j) Xs[xrow[j]][xkk[j]] = xv[j];
+    for (int j = 0; j < XPT; ++j) Xs[rbase + 8 * j][kk] = xv[j];
     __syncthreads();
     if (c + 1 < c_hi) load(c + 1);          // in flight under this chunk's MFMAs
 #pragma unroll
