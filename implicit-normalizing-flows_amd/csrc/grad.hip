@@ -420,7 +420,8 @@ static bool wgrad_valu3r_enabled() {
 
 int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
-  if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0) {
+  if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(a.G) & 15) == 0) {   // float4 loads of G rows
     const bool three = a.ks == 3 && a.x_sample % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0 &&
                        wgrad_valu3_enabled();
     const int nb = three ? (a.N / 3 + 255) / 256 : (a.N + 255) / 256;

@@ -275,9 +275,22 @@ def net_entries(seq):
     return entries
 
 
+class _NativeCache(dict):
+    """Per-module cache of engine nets.  Not copied or pickled with the module: a deep copy (or an
+    unpickled module) builds its own engine nets from its own parameter tensors on first use."""
+
+    def __deepcopy__(self, memo):
+        return _NativeCache()
+
+    def __reduce__(self):
+        return (_NativeCache, ())
+
+
 def native_net(module, shape, device):
     """Cached NativeNet for `module` acting on per-sample `shape` on `device`."""
-    cache = module.__dict__.setdefault('_inf_native', {})
+    cache = module.__dict__.get('_inf_native')
+    if not isinstance(cache, _NativeCache):
+        cache = module.__dict__['_inf_native'] = _NativeCache()
     key = (torch.device(device).index, tuple(shape))
     net = cache.get(key) or cache.get((key[0], (int(torch.Size(shape).numel()),)))
     if net is not None and net.current_ptrs() == net.ptrs:

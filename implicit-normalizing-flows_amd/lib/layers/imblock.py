@@ -108,6 +108,14 @@ class _MemEffLogDet(torch.autograd.Function):
         return (None, grad_x * dL) + tuple(grads)
 
 
+def _engine_result(res, module, what):
+    """netgrad returns None when the engine declines a net that passed _engine_grads' type check."""
+    if res is None:
+        raise _hip.HipError('%s: the MI355X engine does not support the parameter gradients of %r'
+                            % (what, module))
+    return res
+
+
 class _Recompute(torch.autograd.Function):
     """z = (f_x(x0) - f_z(z*)) + x0 with x0, z* constants (implicit_block.py:226-227): the values come from
     the engine's forward, the parameter gradients from inf_net_param_grad (d/dtheta_x of grad . f_x(x0),
@@ -125,8 +133,10 @@ class _Recompute(torch.autograd.Function):
     def backward(ctx, grad):
         x0, z_star = ctx.saved_tensors
         blk = ctx.blk
-        gx, _ = netgrad.param_grads(ctx.nx, blk.nnet_x, x0, grad.contiguous())
-        gz, _ = netgrad.param_grads(ctx.nz, blk.nnet_z, z_star, (-grad).contiguous())
+        gx, _ = _engine_result(netgrad.param_grads(ctx.nx, blk.nnet_x, x0, grad.contiguous()), blk.nnet_x,
+                               'inf_net_param_grad')
+        gz, _ = _engine_result(netgrad.param_grads(ctx.nz, blk.nnet_z, z_star, (-grad).contiguous()), blk.nnet_z,
+                               'inf_net_param_grad')
         px = list(blk.nnet_x.parameters())
         pz = list(blk.nnet_z.parameters())
         out = [gx.get(p) for p in px] + [gz.get(p) for p in pz]
@@ -140,7 +150,8 @@ class _MemEffNeumannNative(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, native, module, w, eps, *params):
-        value, grads, gx = netgrad.surrogate_grads(native, module, x.detach(), w, eps)
+        value, grads, gx = _engine_result(netgrad.surrogate_grads(native, module, x.detach(), w, eps), module,
+                                          'inf_net_surrogate_grad')
         ctx.grads = [grads.get(p) for p in params]
         ctx.save_for_backward(gx)
         return value
@@ -526,8 +537,9 @@ class imBlock(nn.Module):
         self.last_n_power_series = n_ps
         if self.training and self.n_power_series is None:
             solvers.fill_from_host(self.last_n_samples, ns)   # (no pageable H2D copy: it would drain the stream)
-            self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
-            self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
+            estimator = logdetgrad.detach()     # implicit_block.py:347
+            self.last_firmom.copy_(torch.mean(estimator).view(1))
+            self.last_secmom.copy_(torch.mean(estimator ** 2).view(1))
         return logdetgrad.view(-1, 1)
 
     def extra_repr(self):

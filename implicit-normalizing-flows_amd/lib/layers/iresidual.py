@@ -221,8 +221,9 @@ class iResBlock(nn.Module):
         """Moment buffers in training (iresblock.py:159-163)."""
         if self.training and self.n_power_series is None and ns is not None:
             solvers.fill_from_host(self.last_n_samples, ns)   # (no pageable H2D copy: it would drain the stream)
-            self.last_firmom.copy_(torch.mean(logdetgrad).view(1))
-            self.last_secmom.copy_(torch.mean(logdetgrad ** 2).view(1))
+            estimator = logdetgrad.detach()     # iresblock.py:159 (estimator = logdetgrad.detach())
+            self.last_firmom.copy_(torch.mean(estimator).view(1))
+            self.last_secmom.copy_(torch.mean(estimator ** 2).view(1))
         return logdetgrad
 
     def extra_repr(self):

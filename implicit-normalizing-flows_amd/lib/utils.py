@@ -43,15 +43,20 @@ class ExponentialMovingAverage(object):
             for name, param in other_ema.shadow_params.items():
                 self.shadow_params[name].copy_(param)
 
+    # Parameters are written with an in-place copy on the parameter itself (not through .data), so
+    # their version counters advance and the engine re-packs the nets on the next forward
+    # (_hip.NativeNet.refresh_if_needed keys on (data_ptr, _version)).
     def replace_with_ema(self):
-        for name, param in self.module.named_parameters():
-            param.data.copy_(self.shadow_params[name])
+        with torch.no_grad():
+            for name, param in self.module.named_parameters():
+                param.copy_(self.shadow_params[name])
 
     def swap(self):
-        for name, param in self.module.named_parameters():
-            tmp = self.shadow_params[name].clone()
-            self.shadow_params[name].copy_(param.data)
-            param.data.copy_(tmp)
+        with torch.no_grad():
+            for name, param in self.module.named_parameters():
+                tmp = self.shadow_params[name].clone()
+                self.shadow_params[name].copy_(param)
+                param.copy_(tmp)
 
     def state_dict(self):
         return {'decay': float(self.decay), 'shadow_params': {k: v.detach().cpu() for k, v in self.shadow_params.items()}}
@@ -66,20 +71,23 @@ class ExponentialMovingAverage(object):
                                                             self.module.__class__.__name__, self.nparams)
 
 
-def update_lipschitz(model):
+def update_lipschitz(model, skip_frozen_copies=False):
     """compute_weight(update=True) on every InducedNorm conv / linear of `model` (train_img.py:786-792),
     run after each optimiser step; on CUDA each call is one engine power iteration (power.hip).
 
-    The imBlocks' frozen copies (nnet_x_copy / nnet_z_copy) are skipped: the next forward overwrites
-    every one of their parameters and buffers from nnet_x / nnet_z (implicit_block.py:228-229), so
-    updating them, as the reference's walk over model.modules() does, has no observable effect."""
+    Like the reference's walk over model.modules(), this includes the imBlocks' frozen copies
+    (nnet_x_copy / nnet_z_copy), so the u / v / scale buffers of a checkpoint saved after a step match
+    the reference's.  skip_frozen_copies=True leaves the copies out: the next forward overwrites every
+    one of their parameters and buffers from nnet_x / nnet_z (implicit_block.py:228-229), so the loss
+    trajectory is unchanged and only a state_dict taken between the step and the next forward differs."""
     from .layers.base import InducedNormConv2d, InducedNormLinear
     skip = set()
-    for m in model.modules():
-        for name in ('nnet_x_copy', 'nnet_z_copy'):
-            cp = getattr(m, name, None)
-            if isinstance(cp, torch.nn.Module):
-                skip.update(id(c) for c in cp.modules())
+    if skip_frozen_copies:
+        for m in model.modules():
+            for name in ('nnet_x_copy', 'nnet_z_copy'):
+                cp = getattr(m, name, None)
+                if isinstance(cp, torch.nn.Module):
+                    skip.update(id(c) for c in cp.modules())
     with torch.no_grad():
         for m in model.modules():
             if id(m) not in skip and isinstance(m, (InducedNormConv2d, InducedNormLinear)):

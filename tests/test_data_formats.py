@@ -70,3 +70,18 @@ def test_ema_and_checkpoint_roundtrip(tmp_path):
     assert ck['epoch'] == 3
     q0 = dict(m2.named_parameters())[name]
     np.testing.assert_allclose(q0.detach().numpy(), ema.shadow_params[name].numpy())
+
+
+def test_ema_swap_and_replace_bump_parameter_versions():
+    """The engine re-packs a net when a parameter's (data_ptr, _version) stamp changes, so EMA writes
+    must go through the parameter (not .data)."""
+    m = build_flow(syn.CIFAR10_SMALL, 2)
+    ema = utils.ExponentialMovingAverage(m, decay=0.5)
+    ema.apply()
+    params = list(m.parameters())
+    v0 = [p._version for p in params]
+    ema.swap()
+    v1 = [p._version for p in params]
+    assert all(b > a for a, b in zip(v0, v1))
+    ema.replace_with_ema()
+    assert all(c > b for b, c in zip(v1, [p._version for p in params]))

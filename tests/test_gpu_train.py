@@ -186,3 +186,45 @@ def test_engine_param_and_surrogate_grads_match_autograd(C, hid, preact, H):
         r = torch.zeros_like(p) if r is None else r
         _check_param(grads2[p], r, 'surrogate param %s' % (tuple(p.shape),))
     _check_param(gx2, ref2[-1], 'surrogate x')
+
+
+def test_ema_swap_repacks_engine_weights_and_model_deepcopies():
+    """After a training step, ema.swap() twice must leave the engine holding the live weights (the swap
+    writes bump the parameters' version counters, so inf_net_refresh re-packs), and the model must
+    deep-copy (moment buffers are filled from the detached estimator, implicit_block.py:347)."""
+    import copy
+    from lib.utils import ExponentialMovingAverage
+    arch = syn.CIFAR10_SMALL
+    B = 2
+    m = build_flow(arch, B)
+    m.load_state_dict(syn.make_state_dict(arch, 0), strict=True)
+    m = m.to(DEV).train()
+    ema = ExponentialMovingAverage(m, decay=0.5)
+    ema.apply()
+    set_probe_mode('device', seed=3)
+    x = syn.image_batch(B, seed=2).to(DEV)
+    np.random.seed(0)
+    loss, _, _ = image_bits_per_dim_graph(m, x, arch['nvals'])
+    loss.backward()
+    with torch.no_grad():
+        for p in m.parameters():
+            if p.grad is not None:
+                p.add_(p.grad, alpha=-1e-2)
+    ema.apply()                                   # shadow now differs from the live weights
+    m.eval()
+    with torch.no_grad():
+        ema.swap()
+        m(x, 0)                                   # engine packs the EMA weights
+        ema.swap()
+        np.random.seed(0)
+        set_probe_mode('device', seed=3)
+        _, lp_live = m(x, 0)
+        fresh = copy.deepcopy(m)                  # deep copy: fresh native nets, packed from scratch
+        for blk in imblocks(fresh):
+            assert not blk.nnet_x.__dict__.get('_inf_native')
+        np.random.seed(0)
+        set_probe_mode('device', seed=3)
+        _, lp_fresh = fresh(x, 0)
+    torch.cuda.synchronize()
+    set_probe_mode('reference')
+    torch.testing.assert_close(lp_live, lp_fresh, rtol=0, atol=1e-5)

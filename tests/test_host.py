@@ -116,21 +116,26 @@ def test_copy_refresh_matches_load_state_dict():
         assert not p.requires_grad
 
 
-def test_update_lipschitz_walks_nets_not_copies(monkeypatch):
-    """lib.utils.update_lipschitz (train_img.py:786-792) updates every InducedNorm layer of the nets and
-    skips the frozen copies, whose tensors the next forward overwrites (implicit_block.py:228-229)."""
+def test_update_lipschitz_walks_nets_and_copies(monkeypatch):
+    """lib.utils.update_lipschitz (train_img.py:786-792) updates every InducedNorm layer of the model, the
+    frozen copies included (as the reference's walk over model.modules() does), each once;
+    skip_frozen_copies=True leaves the copies out (their tensors the next forward overwrites,
+    implicit_block.py:228-229)."""
     from lib.layers import base
     from lib.utils import update_lipschitz
     m = build_flow(syn.CIFAR10_SMALL, 2)
     seen = []
     for cls in (base.InducedNormConv2d, base.InducedNormLinear):
         monkeypatch.setattr(cls, 'compute_weight', lambda self, update=True, **kw: seen.append(id(self)))
-    update_lipschitz(m)
     kinds = (base.InducedNormConv2d, base.InducedNormLinear)
     want, copies = set(), set()
     for blk in imblocks(m):
         want.update(id(c) for net in (blk.nnet_x, blk.nnet_z) for c in net.modules() if isinstance(c, kinds))
         copies.update(id(c) for net in (blk.nnet_x_copy, blk.nnet_z_copy) for c in net.modules()
                       if isinstance(c, kinds))
-    assert want and len(seen) == len(set(seen))
-    assert set(seen) == want and not (set(seen) & copies)
+    update_lipschitz(m)
+    assert want and copies and len(seen) == len(set(seen))
+    assert set(seen) == want | copies
+    seen.clear()
+    update_lipschitz(m, skip_frozen_copies=True)
+    assert set(seen) == want and len(seen) == len(want)
