@@ -392,8 +392,30 @@ int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
   INF_HIP(hipEventRecord(sl->ev, s));
   return INF_OK;
 }
+// Host wait on a readback event.  A blocking hipEventSynchronize that has to wait long (e.g. behind a whole
+// log-det series) lets the runtime put the thread to sleep, and its wake-up comes late, with the GPU idle
+// and nothing else queued; polling hipEventQuery keeps the host turnaround at the copy's latency.
+// INFLOW_BLOCKING_WAIT=1 restores the blocking wait.
+int host_wait(hipEvent_t ev) {
+  static const bool blocking = [] {
+    const char* e = getenv("INFLOW_BLOCKING_WAIT");
+    return e && e[0] == '1';
+  }();
+  if (blocking) {
+    INF_HIP(hipEventSynchronize(ev));
+    return INF_OK;
+  }
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return INF_OK;
+    if (q != hipErrorNotReady) {
+      set_hip_error(q);
+      return INF_ERR_HIP;
+    }
+  }
+}
 int wait_sumsq(SumsSlot* sl, int B, std::vector<double>& host_sumsq) {
-  INF_HIP(hipEventSynchronize(sl->ev));
+  INF_TRY(host_wait(sl->ev));
   memcpy(host_sumsq.data(), sl->host, sizeof(double) * B);
   return INF_OK;
 }

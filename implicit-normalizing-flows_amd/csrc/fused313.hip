@@ -43,6 +43,19 @@ namespace inf {
 //                    next to a 64-pixel activation tile (9C up to ~1.7K tap rows: CelebA-HQ 64x64 and
 //                    32x32 scales)
 constexpr int LDS_FULL = 40960, LDS_HALF = 20480;
+constexpr int TSLOTS = 32;
+#ifndef PB_BPIPE
+#define PB_BPIPE 1   // phase-B B operand split one K tile ahead (2-3 % per series term at s0/s1)
+#endif
+#ifndef PB_SCHED
+#define PB_SCHED 4   // with PB_BPIPE: sched_group_barrier interleave, this many VALU per MFMA
+#endif
+#ifndef PB_PRIO
+#define PB_PRIO 0    // phase-B issue priority: 1 alternate per K tile between SIMD partners, 2 younger half
+#endif
+#ifndef PB_DEPTH
+#define PB_DEPTH 2   // phase-B weight prefetch ring (K tiles); 2 = ping-pong
+#endif   // INFLOW_FUSED_TIMING stamps per workgroup
 
 __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   const f32x4 v0 = *reinterpret_cast<const f32x4*>(base);
@@ -68,9 +81,20 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
 #define STAMP(i_)                                                                            \
   do {                                                                                       \
-    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * 8 + (i_)] = __builtin_amdgcn_s_memtime(); \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  // per-wave stamps (lane 0 of every wave): slot 8 + w at its phase-B end, 16 + w once its epilogue-B
+  // multiplier has arrived
+#define WSTAMP(base_)                                                                         \
+  do {                                                                                       \
+    if (pr.tbuf && (threadIdx.x & 63) == 0) {                                                \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
+      pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + (threadIdx.x >> 6)] = t_;                \
+      if (NW == 4) pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + 4 + (threadIdx.x >> 6)] = t_; \
+    }                                                                                        \
   } while (0)
   STAMP(0);
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
   float* t = smem;                                  // [HID][64] activation tile
   int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
   float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
@@ -427,34 +451,94 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       o[1] = q[64];
       o[2] = q[128];
     };
-    auto tileB = [&](int kt, const u32x4 (&af)[TM][3]) {
+    // B operand of a K tile: this lane's 8 k-values of its NB pixel columns from the LDS tile, split
+    struct BOp { u32x4 h[NB], m[NB], l[NB]; };
+    auto bprep = [&](int kt, BOp& o) {
       const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
-      u32x4 bh[NB], bm[NB], bl[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         float x[8];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) x[kk] = tb[kk * F_BN + 32 * b];
-        split3(x, bh[b], bm[b], bl[b]);
+#ifdef INFLOW_EXP_NOSPLIT      // diagnostic build only (wrong results): no B-operand split VALU
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o.h[b][j] = __builtin_amdgcn_perm(__float_as_uint(x[2 * j + 1]), __float_as_uint(x[2 * j]), 0x07060302u);
+          o.m[b][j] = 0u;
+          o.l[b][j] = 0u;
+        }
+#else
+        split3(x, o.h[b], o.m[b], o.l[b]);
+#endif
       }
+    };
+    auto bmma = [&](const u32x4 (&af)[TM][3], const BOp& o) {
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], bh[b], bm[b], bl[b], acc[m][b]);
+        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], o.h[b], o.m[b], o.l[b], acc[m][b]);
     };
-    u32x4 a0[TM][3], a1[TM][3];
+    // weight operand ring: PB_DEPTH K tiles of A fragments, the next D-1 in flight behind the one in use;
+    // with PB_BPIPE the B operand of the next K tile is read and split while this tile's MFMAs issue
+    constexpr int D = (F_LDS_FLOATS == LDS_HALF) ? 2 : PB_DEPTH;
+    constexpr bool BPIPE = PB_BPIPE && F_LDS_FLOATS != LDS_HALF;
+    static_assert(nkt % D == 0 && D % 2 == 0, "phase-B K tiles must be a multiple of the prefetch depth");
+    u32x4 ab[D][TM][3];
+    BOp bo[BPIPE ? 2 : 1];
 #pragma unroll
-    for (int m = 0; m < TM; ++m) ld3(m, 0, a0[m]);
-    for (int kt = 0; kt < nkt; kt += 2) {
+    for (int d = 0; d + 1 < D; ++d)
 #pragma unroll
-      for (int m = 0; m < TM; ++m) ld3(m, kt + 1, a1[m]);
-      tileB(kt, a0);
-      if (kt + 2 < nkt) {
+      for (int m = 0; m < TM; ++m) ld3(m, d, ab[d][m]);
+    if constexpr (BPIPE) bprep(0, bo[0]);
+#if PB_PRIO == 2
+    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);      // the younger half wins arbitration
+#endif
+    for (int kt = 0; kt < nkt; kt += D) {
 #pragma unroll
-        for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
+      for (int d = 0; d < D; ++d) {
+        const int kn = kt + d + D - 1;
+#ifdef INFLOW_EXP_NOWLOAD       // diagnostic build only (wrong results): no weight loads after the prologue
+        if (kn < D)
+#elif PB_SCHED
+        if (true)      // (the last D-1 steps reload the last K tile: one straight-line block per step)
+#else
+        if (kn < nkt)
+#endif
+        {
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ld3(m, min(kn, nkt - 1), ab[(d + D - 1) % D][m]);
+        }
+        if constexpr (BPIPE) {
+#if PB_SCHED
+#if PB_PRIO == 1
+          // the two waves of a SIMD take turns at issue priority, so neither is left alone at the end
+          if (((kt + d) ^ (wid >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+#endif
+          bprep(min(kt + d + 1, nkt - 1), bo[(d + 1) % 2]);   // (clamped: one straight-line block per step)
+          bmma(ab[d], bo[d % 2]);
+          // interleave: the weight loads and next tile's LDS reads first, then each MFMA followed by ~4 VALU
+          __builtin_amdgcn_sched_group_barrier(0x020, TM * 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 * NB, 0);
+#pragma unroll
+          for (int i = 0; i < 6 * TM * NB - 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, PB_SCHED, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#else
+          if (kt + d + 1 < nkt) bprep(kt + d + 1, bo[(d + 1) % 2]);
+          bmma(ab[d], bo[d % 2]);
+#endif
+        } else {
+          bprep(kt + d, bo[0]);
+          bmma(ab[d], bo[0]);
+        }
       }
-      tileB(kt + 1, a1);
     }
+#if PB_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   } else {
     constexpr int nkt = HID / 16;
     auto tileB = [&](int kt, const float (&af)[TM][8]) {
@@ -487,6 +571,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }
   }
   STAMP(4);
+  WSTAMP(8);
   if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) {
     const float sp2 = softplus_f(*a.beta2);
 #pragma unroll
@@ -523,6 +608,15 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           if constexpr (MODE == MODE_VJP) acc[m][b][r] = acc[m][b][r] * dmul[m][b][r];
           else acc[m][b][r] = swish_f(acc[m][b][r] + a.b2[o], sp2);
         }
+    if (pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
+      float s_ = 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) s_ += acc[m][b][0];
+      if (s_ == 12345.678f) pr.tbuf[0] = 0;
+      WSTAMP(16);
+    }
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < TM; ++m)
@@ -730,7 +824,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }   // rounds
   }
   STAMP(7);
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
 #undef STAMP
+#undef WSTAMP
 }
 
 template <int TM, int MODE, int SPL>
@@ -779,6 +875,11 @@ int net313_supported(int hid, int C, int H, int W) {
 // ---- INFLOW_FUSED_TIMING (development): per-phase s_memtime deltas of wave 0, averaged per kernel
 struct TimingAcc {
   double sum[7] = {0, 0, 0, 0, 0, 0, 0};
+  double bmin = 0, bmax = 0, dmax = 0;   // per-wave phase-B ends / multiplier arrivals, relative to stamp 3
+  double bw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double rt = 0, mt = 0;                 // wave 0's lifetime in s_memrealtime (100 MHz) and s_memtime ticks
+  double span = 0;                       // per call: latest end - earliest start over its workgroups (realtime)
+  long ncalls = 0;
   long n = 0;
 };
 static std::map<std::string, TimingAcc>& timing_map() {
@@ -790,7 +891,12 @@ static void timing_report() {
   for (auto& kv : timing_map()) {
     fprintf(stderr, "[timing] %-28s n=%6ld", kv.first.c_str(), kv.second.n);
     for (int i = 0; i < 7; ++i) fprintf(stderr, " %s %.0f", names[i], kv.second.sum[i] / kv.second.n);
-    fprintf(stderr, "\n");
+    fprintf(stderr, " | waves: phaseB end min %.0f max %.0f, epiB multiplier ready max %.0f | per wave",
+            kv.second.bmin / kv.second.n, kv.second.bmax / kv.second.n, kv.second.dmax / kv.second.n);
+    for (int v = 0; v < 8; ++v) fprintf(stderr, " %.0f", kv.second.bw[v] / kv.second.n);
+    fprintf(stderr, " | clock %.2f GHz, workgroup %.2f us, per call: workgroup-time / 256 CUs %.1f us, span %.1f us\n",
+            kv.second.mt / kv.second.rt * 0.1, kv.second.rt / kv.second.n * 0.01,
+            kv.second.rt * 0.01 / 256.0 / kv.second.ncalls, kv.second.span * 0.01 / kv.second.ncalls);
   }
 }
 static unsigned long long* g_tbuf = nullptr;
@@ -798,7 +904,7 @@ static long g_tbuf_n = 0;
 static unsigned long long* timing_buf(long nwg) {
   if (nwg > g_tbuf_n) {
     if (g_tbuf) (void)hipFree(g_tbuf);
-    if (hipMallocManaged(&g_tbuf, nwg * 8 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMallocManaged(&g_tbuf, nwg * TSLOTS * sizeof(unsigned long long)) != hipSuccess) return nullptr;
     g_tbuf_n = nwg;
     static bool reg = false;
     if (!reg) { atexit(timing_report); reg = true; }
@@ -809,13 +915,34 @@ static void timing_collect(const char* key, long nwg, hipStream_t s) {
   if (!g_tbuf) return;
   (void)hipStreamSynchronize(s);
   TimingAcc& acc = timing_map()[key];
+  unsigned long long lo = ~0ull, hi = 0;
   for (long w = 0; w < nwg; ++w) {
-    const unsigned long long* t = g_tbuf + w * 8;
+    const unsigned long long* t = g_tbuf + w * TSLOTS;
     bool ok = true;
     for (int i = 1; i < 8; ++i) ok = ok && t[i] >= t[i - 1];
     if (!ok) continue;   // e.g. SAVE mode: no phase C stamps
     for (int i = 0; i < 7; ++i) acc.sum[i] += (double)(t[i + 1] - t[i]);
+    double bmin = 1e30, bmax = 0, dmax = 0;
+    for (int v = 0; v < 8; ++v) {
+      bmin = fmin(bmin, (double)t[8 + v] - (double)t[3]);
+      bmax = fmax(bmax, (double)t[8 + v] - (double)t[3]);
+      dmax = fmax(dmax, (double)t[16 + v] - (double)t[3]);
+      acc.bw[v] += (double)t[8 + v] - (double)t[3];
+    }
+    if (t[25] > t[24]) {
+      acc.rt += (double)(t[25] - t[24]);
+      acc.mt += (double)(t[7] - t[0]);
+      lo = t[24] < lo ? t[24] : lo;
+      hi = t[25] > hi ? t[25] : hi;
+    }
+    acc.bmin += bmin;
+    acc.bmax += bmax;
+    acc.dmax += dmax;
     acc.n += 1;
+  }
+  if (hi > lo) {
+    acc.span += (double)(hi - lo);
+    acc.ncalls += 1;
   }
 }
 

@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libinflow.so')
-LIB_PATH = os.environ.get('INFLOW_LIB', LIB_PATH)   # development knob: an alternative build
+LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alternative build
 
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)

@@ -44,12 +44,38 @@ def shard(n_total, rank, world_size):
 
 
 def global_logpx_sum(logpx_local):
-    """All-reduce [sum log p(x), N] (fp64) over the default group; returns python floats."""
-    t = torch.stack([logpx_local.double().sum(), torch.tensor(float(logpx_local.numel()), dtype=torch.float64,
-                                                                  device=logpx_local.device)])
+    """All-reduce [sum log p(x), N] (fp64) over the default group; returns python floats.
+
+    The pair is built on the device (a fill, not a pageable host-to-device copy, which would wait for the
+    whole queue) and read back with one 16-byte copy."""
+    t = torch.empty(2, dtype=torch.float64, device=logpx_local.device)
+    t[0] = logpx_local.sum(dtype=torch.float64)
+    t[1].fill_(float(logpx_local.numel()))
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t[0]), float(t[1])
+    return _readback(t)
+
+
+_PINNED = {}
+
+
+def _readback(t):
+    """Two fp64 device values -> python floats through a pinned host buffer (an asynchronous copy plus an event
+    wait, polled rather than blocking: after a long wait the blocking form returns late, with the GPU idle)."""
+    if t.device.type != 'cuda':
+        return tuple(t.tolist())
+    buf = _PINNED.get(t.device.index)
+    if buf is None:
+        buf = _PINNED[t.device.index] = torch.empty(2, dtype=torch.float64, pin_memory=True)
+    buf.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    if os.environ.get('INFLOW_BLOCKING_WAIT', '') == '1':
+        ev.synchronize()
+    else:                      # poll: a long blocking wait wakes up late (see engine.hip host_wait)
+        while not ev.query():
+            pass
+    return float(buf[0]), float(buf[1])
 
 
 def bits_per_dim(sum_logpx, count, ndim):

@@ -1,0 +1,12 @@
+# Build an alternative libinflow.so with extra compile flags on fused313.hip only (A/B experiments):
+#   bash tools/build_alt.sh <name> "<flags>"   ->  gpurun_alt/lib_<name>.so   (run tools/attr.sh <name> on the box)
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+C=$R/implicit-normalizing-flows_amd/csrc
+O=$R/implicit-normalizing-flows_amd/lib/_hip/obj
+mkdir -p $R/gpurun_alt
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=fast $2 -c -o /tmp/alt_$1.o $C/fused313.hip
+objs=""
+for f in $O/*.o; do case $f in */fused313.o) ;; *) objs="$objs $f";; esac; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/gpurun_alt/lib_$1.so /tmp/alt_$1.o $objs
+echo built gpurun_alt/lib_$1.so
