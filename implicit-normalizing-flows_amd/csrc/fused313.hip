@@ -95,10 +95,6 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   } while (0)
   STAMP(0);
   if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
-  float* t = smem;                                  // [HID][64] activation tile
-  int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
-  float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
-
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int P = a.H * a.W;
@@ -113,6 +109,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // K-padding rows of the im2col point at vh[vhn]; phase A reads vh[koff + pix], so the zero run
   // after the halo must cover every pixel offset of the tile: rows * CW floats.
   const int vhz = vhn + rows * CW;
+  float* t = smem;                                  // [HID][F_BN] activation tile
+  int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
+  float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
 
   // split path: phase A's first operand tile is requested before the staging loads (it is an L2 hit and
   // retires long before the staging data, so it costs the staging nothing and phase A starts without a wait)
@@ -491,7 +490,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int m = 0; m < TM; ++m) ld3(m, d, ab[d][m]);
     if constexpr (BPIPE) bprep(0, bo[0]);
 #if PB_PRIO == 2
-    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);      // the younger half wins arbitration
+    if (__builtin_amdgcn_readfirstlane(wid) >= NW / 2) __builtin_amdgcn_s_setprio(1);   // younger half wins
 #endif
     for (int kt = 0; kt < nkt; kt += D) {
 #pragma unroll
@@ -512,7 +511,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #if PB_SCHED
 #if PB_PRIO == 1
           // the two waves of a SIMD take turns at issue priority, so neither is left alone at the end
-          if (((kt + d) ^ (wid >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+          // (wave id through readfirstlane: a scalar branch; a vector condition would run both setprios)
+          if (((kt + d) ^ (__builtin_amdgcn_readfirstlane(wid) >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
 #endif
           bprep(min(kt + d + 1, nkt - 1), bo[(d + 1) % 2]);   // (clamped: one straight-line block per step)
