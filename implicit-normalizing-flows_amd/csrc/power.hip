@@ -14,6 +14,7 @@
 // iterations into no-ops, so the host looks at the flag once per chunk instead of every iteration.
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "kernels.h"
 
@@ -378,6 +379,97 @@ int inf_power_iteration(const InfPowerIterDesc* d, int max_iters, int use_tol, f
   // the count needs no further readback: with the tolerance test the last flag read came after every
   // iteration kernel; without it every iteration runs
   if (iters_used) *iters_used = use_tol ? h.iters : max_iters;
+  return INF_OK;
+}
+
+// ---- many layers at once (update_lipschitz, train_img.py:786-792): the same per-layer iterations and
+// stopping rule, but every unfinished layer's chunk is queued before ONE read-back of all the layers' flags,
+// so the host waits once per chunk (<= 5 times for 30 iterations) instead of once per chunk per layer.
+static size_t pi_layer_bytes(const InfPowerIterDesc* d) {
+  const PIOp op = pi_op(d);
+  return (((size_t)(pi_nu(op) + pi_nv(op)) * sizeof(float) + 255) / 256) * 256 + 3 * PI_NB * sizeof(double) + 256;
+}
+
+size_t inf_power_iteration_batch_workspace_bytes(const InfPowerIterDesc* descs, int n) {
+  if (!descs || n <= 0) return 0;
+  size_t b = ((sizeof(PIState) * (size_t)n + 255) / 256) * 256;
+  for (int i = 0; i < n; ++i) {
+    if (!pi_valid(&descs[i])) return 0;
+    b += pi_layer_bytes(&descs[i]);
+  }
+  return b;
+}
+
+int inf_power_iteration_batch(const InfPowerIterDesc* descs, int n, int max_iters, int use_tol, float atol,
+                              float rtol, int* iters_used, void* ws, size_t ws_bytes, void* stream) {
+  if (!descs || n <= 0 || max_iters < 0) return INF_ERR_INVALID;
+  for (int i = 0; i < n; ++i)
+    if (!pi_valid(&descs[i])) return INF_ERR_INVALID;
+  if (!ws || ws_bytes < inf_power_iteration_batch_workspace_bytes(descs, n)) return INF_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  char* base = reinterpret_cast<char*>(ws);
+  PIState* states = reinterpret_cast<PIState*>(base);
+  char* cur = base + ((sizeof(PIState) * (size_t)n + 255) / 256) * 256;
+  struct Layer {
+    PIOp op;
+    long nu, nv;
+    float *us, *vs;
+    double* scr;
+  };
+  std::vector<Layer> L(n);
+  for (int i = 0; i < n; ++i) {
+    Layer& l = L[i];
+    l.op = pi_op(&descs[i]);
+    l.nu = pi_nu(l.op);
+    l.nv = pi_nv(l.op);
+    l.us = reinterpret_cast<float*>(cur);
+    l.vs = l.us + l.nu;
+    l.scr = reinterpret_cast<double*>(cur + (((size_t)(l.nu + l.nv) * sizeof(float) + 255) / 256) * 256);
+    cur += pi_layer_bytes(&descs[i]);
+    hipLaunchKernelGGL(pi_init, dim3(1), dim3(1), 0, s, states + i, use_tol ? 1 : 0, atol, rtol);
+  }
+  std::vector<PIState> h(n);
+  memset(h.data(), 0, sizeof(PIState) * n);
+  std::vector<char> live(n, 1);
+  int done_iters = 0, chunk = use_tol ? 2 : max_iters;
+  while (done_iters < max_iters) {
+    const int c = std::min(chunk, max_iters - done_iters);
+    for (int i = 0; i < n; ++i) {
+      if (!live[i]) continue;
+      const InfPowerIterDesc& d = descs[i];
+      for (int k = 0; k < c; ++k) {
+        pi_launch_w(L[i].op, d.v, L[i].us, states + i, s);
+        pi_launch_normalize(L[i].us, d.u, L[i].nu, states + i, 0, L[i].scr, s);
+        pi_launch_wt(L[i].op, d.u, L[i].vs, states + i, s);
+        pi_launch_normalize(L[i].vs, d.v, L[i].nv, states + i, 1, L[i].scr, s);
+      }
+    }
+    INF_CHECK_LAUNCH();
+    done_iters += c;
+    chunk = std::min(2 * chunk, 8);
+    if (!use_tol) continue;
+    INF_HIP(hipMemcpyAsync(h.data(), states, sizeof(PIState) * n, hipMemcpyDeviceToHost, s));
+    INF_HIP(hipStreamSynchronize(s));
+    bool any = false;
+    for (int i = 0; i < n; ++i) {
+      if (h[i].done) live[i] = 0;
+      any = any || live[i];
+    }
+    if (!any) break;
+  }
+  for (int i = 0; i < n; ++i) {      // sigma = u . (W v)
+    const InfPowerIterDesc& d = descs[i];
+    pi_launch_w(L[i].op, d.v, L[i].us, nullptr, s);
+    if (L[i].nu < PI_MULTI_MIN) {
+      hipLaunchKernelGGL(pi_sigma, dim3(1), dim3(1024), 0, s, d.u, L[i].us, L[i].nu, states + i, d.scale);
+    } else {
+      hipLaunchKernelGGL(pi_dot_part, dim3(PI_NB), dim3(256), 0, s, d.u, L[i].us, L[i].nu, nullptr, L[i].scr);
+      hipLaunchKernelGGL(pi_sigma_final, dim3(1), dim3(256), 0, s, L[i].scr, PI_NB, states + i, d.scale);
+    }
+  }
+  INF_CHECK_LAUNCH();
+  if (iters_used)
+    for (int i = 0; i < n; ++i) iters_used[i] = use_tol ? h[i].iters : max_iters;
   return INF_OK;
 }
 

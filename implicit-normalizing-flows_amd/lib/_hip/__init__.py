@@ -120,6 +120,10 @@ _SIGS = {
     'inf_power_iteration_workspace_bytes': (ctypes.c_size_t, [ctypes.POINTER(PowerIterDesc)]),
     'inf_power_iteration': (ctypes.c_int, [ctypes.POINTER(PowerIterDesc), ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                            ctypes.c_float, ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),
+    'inf_power_iteration_batch_workspace_bytes': (ctypes.c_size_t, [ctypes.POINTER(PowerIterDesc), ctypes.c_int]),
+    'inf_power_iteration_batch': (ctypes.c_int, [ctypes.POINTER(PowerIterDesc), ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                                 ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),
 }
 EXPORTS = tuple(_SIGS)
 

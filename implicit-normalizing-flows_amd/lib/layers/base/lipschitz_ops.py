@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.nn.init as init
 
-__all__ = ['InducedNormConv2d', 'InducedNormLinear', 'get_conv2d', 'get_linear']
+__all__ = ['InducedNormConv2d', 'InducedNormLinear', 'get_conv2d', 'get_linear', 'batch_power_update']
 
 
 def _unit(t):
@@ -56,6 +56,53 @@ def _native_power_iteration(kind, cin, cout, ksize, hw, W, u, v, scale, itrs, at
     for t in (u, v, scale):
         torch.autograd.graph.increment_version(t)
     return used.value
+
+
+def batch_power_update(modules):
+    """compute_weight(update=True) for many InducedNorm layers on one device: one engine call
+    (inf_power_iteration_batch) per tolerance setting, so the host reads the convergence flags once per
+    speculative chunk for all layers.  Same per-layer iterations, stopping rule and results as calling
+    compute_weight(update=True) on each; layers not yet initialised take that per-layer path."""
+    from ... import _hip
+    groups, rest = {}, []
+    for m in modules:
+        if not m.weight.is_cuda:
+            rest.append(m)
+            continue
+        if isinstance(m, InducedNormConv2d):
+            if not m._initialized_host():
+                rest.append(m)
+                continue
+            k = m.kernel_size[0]
+            if m.kernel_size != (k, k) or m.stride != (1, 1) or m.padding != (k // 2, k // 2):
+                rest.append(m)
+                continue
+            hw = (1, 1) if m.is_1x1 else m._hw()
+            d = (1, m.in_channels, m.out_channels, k, hw)
+        else:
+            d = (2, m.in_features, m.out_features, 1, (1, 1))
+        n_iterations, atol, rtol = m.n_iterations, m.atol, m.rtol   # compute_weight's defaults
+        itrs = _iteration_budget(n_iterations, atol, rtol)
+        key = (m.weight.device, itrs, n_iterations is None, atol, rtol)
+        groups.setdefault(key, []).append((m, d))
+    for m in rest:
+        m.compute_weight(update=True)
+    lib = _hip.load() if groups else None
+    for (dev, itrs, use_tol, atol, rtol), items in groups.items():
+        descs = (_hip.PowerIterDesc * len(items))()
+        for j, (m, (kind, cin, cout, ks, hw)) in enumerate(items):
+            descs[j] = _hip.PowerIterDesc(kind=kind, cin=cin, cout=cout, ksize=ks, height=hw[0], width=hw[1],
+                                          weight=m.weight.data_ptr(), u=m.u.data_ptr(), v=m.v.data_ptr(),
+                                          scale=m.scale.data_ptr())
+        used = (ctypes.c_int * len(items))()
+        ws = _hip.workspace(dev, lib.inf_power_iteration_batch_workspace_bytes(descs, len(items)))
+        _hip.check(lib.inf_power_iteration_batch(descs, len(items), int(itrs), int(bool(use_tol)), float(atol or 0.),
+                                                 float(rtol or 0.), used, _hip.ptr(ws), ws.numel(),
+                                                 _hip.stream_of(m.weight)), 'inf_power_iteration_batch')
+        for j, (m, _) in enumerate(items):
+            m.last_power_iters = used[j]
+            for t in (m.u, m.v, m.scale):
+                torch.autograd.graph.increment_version(t)
 
 
 def _iteration_budget(n_iterations, atol, rtol):
@@ -171,7 +218,23 @@ class InducedNormConv2d(nn.Module):
         return self.kernel_size == (1, 1)
 
     def _hw(self):
-        return int(self.spatial_dims[0].item()), int(self.spatial_dims[1].item())
+        """spatial_dims as ints; read from the device only when the buffer changed (no sync per call)."""
+        t = self.spatial_dims
+        key = (t.data_ptr(), t._version)
+        c = self.__dict__.get('_hw_cache')
+        if c is None or c[0] != key:
+            h, w = t.tolist()
+            c = self.__dict__['_hw_cache'] = (key, (int(h), int(w)))
+        return c[1]
+
+    def _initialized_host(self):
+        """bool(self.initialized) without a device sync once it is known to be set."""
+        t = self.initialized
+        key = (t.data_ptr(), t._version)
+        c = self.__dict__.get('_init_cache')
+        if c is None or c[0] != key:
+            c = self.__dict__['_init_cache'] = (key, bool(t.item()))
+        return c[1]
 
     def _conv_ops(self, W):
         c = self.in_channels
@@ -197,7 +260,7 @@ class InducedNormConv2d(nn.Module):
             self.compute_weight(True)
 
     def compute_weight(self, update=True, n_iterations=None, atol=None, rtol=None):
-        if not self.initialized:
+        if not self._initialized_host():
             self._initialize_u_v()
         n_iterations = self.n_iterations if n_iterations is None else n_iterations
         atol = self.atol if atol is None else atol
@@ -246,7 +309,7 @@ class InducedNormConv2d(nn.Module):
         return torch.dot(u, fwd(v))
 
     def forward(self, x):
-        if not self.initialized:
+        if not self._initialized_host():
             self.spatial_dims.copy_(torch.tensor(x.shape[2:4]).to(self.spatial_dims))
         return F.conv2d(x, self.compute_weight(update=False), self.bias, self.stride, self.padding, 1, 1)
 

@@ -88,10 +88,11 @@ def update_lipschitz(model, skip_frozen_copies=False):
                 cp = getattr(m, name, None)
                 if isinstance(cp, torch.nn.Module):
                     skip.update(id(c) for c in cp.modules())
+    from .layers.base.lipschitz_ops import batch_power_update
     with torch.no_grad():
-        for m in model.modules():
-            if id(m) not in skip and isinstance(m, (InducedNormConv2d, InducedNormLinear)):
-                m.compute_weight(update=True)
+        mods = [m for m in model.modules()
+                if id(m) not in skip and isinstance(m, (InducedNormConv2d, InducedNormLinear))]
+        batch_power_update(mods)     # device layers: one engine call, flags read once per chunk for all
 
 
 def save_checkpoint(path, model, ema=None, **extra):

@@ -214,6 +214,12 @@ size_t inf_power_iteration_workspace_bytes(const InfPowerIterDesc* desc);
  * v.  iters_used (may be NULL) receives the count. */
 int inf_power_iteration(const InfPowerIterDesc* desc, int max_iters, int use_tol, float atol, float rtol,
                         int* iters_used, void* ws, size_t ws_bytes, void* stream);
+/* The same for n layers in one call (update_lipschitz over a model, train_img.py:786-792): per-layer
+ * iterations and stopping rule unchanged; all unfinished layers advance one speculative chunk between
+ * the host's flag reads.  iters_used (may be NULL) receives n counts. */
+size_t inf_power_iteration_batch_workspace_bytes(const InfPowerIterDesc* descs, int n);
+int inf_power_iteration_batch(const InfPowerIterDesc* descs, int n, int max_iters, int use_tol, float atol,
+                              float rtol, int* iters_used, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- parameter gradients (training path; conv nets with swish activations) ------------------------
  * Device buffers per weight layer l (in order; NULL entries / arrays are skipped): dW[l] the gradient of

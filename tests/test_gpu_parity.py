@@ -361,6 +361,38 @@ def test_power_iteration_matches_host(kind):
     np.testing.assert_allclose(w_dev.cpu().numpy(), w_host.detach().numpy(), rtol=1e-5, atol=1e-7)
 
 
+def test_update_lipschitz_batch_matches_per_layer():
+    """lib.utils.update_lipschitz (one inf_power_iteration_batch call for all layers) vs compute_weight(update=True)
+    layer by layer (inf_power_iteration) on a copy: identical iteration counts, u, v and scale (bit for bit:
+    the same kernels in the same order per layer)."""
+    from lib.layers import base
+    from lib.utils import update_lipschitz
+    arch = syn.CIFAR10_SMALL
+    m = build_flow(arch, 2)
+    m.load_state_dict(syn.make_state_dict(arch, 0), strict=True)
+    m = m.to(DEV)
+    torch.manual_seed(3)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.02 * torch.randn_like(p))          # as after an optimiser step
+    ref = copy.deepcopy(m)
+    kinds = (base.InducedNormConv2d, base.InducedNormLinear)
+    update_lipschitz(m)
+    with torch.no_grad():
+        for q in ref.modules():
+            if isinstance(q, kinds):
+                q.compute_weight(update=True)
+    torch.cuda.synchronize()
+    n = 0
+    for a, b in zip(m.modules(), ref.modules()):
+        if isinstance(a, kinds):
+            assert a.last_power_iters == b.last_power_iters
+            for name in ('u', 'v', 'scale'):
+                assert torch.equal(getattr(a, name), getattr(b, name)), name
+            n += 1
+    assert n > 0
+
+
 @pytest.mark.parametrize('C,H,hid,B', [(48, 64, 512, 2), (192, 32, 512, 2), (3, 32, 256, 8), (12, 16, 256, 2)])
 @pytest.mark.parametrize('mfma', [0, 1])
 def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):

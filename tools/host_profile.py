@@ -1,5 +1,6 @@
-"""Host-side (Python) profile of the eval step: cProfile over K steps of the CIFAR bench workload.
-    python tools/host_profile.py [--steps 5]"""
+"""Host-side (Python) profile of the eval step (or, with --train, the full training step of bench.py --mode
+train): cProfile over K steps of the CIFAR bench workload.
+    python tools/host_profile.py [--steps 5] [--train]"""
 import cProfile
 import os
 import pstats
@@ -28,7 +29,28 @@ set_probe_mode('device', seed=1)
 np.random.seed(0)
 
 
+TRAIN = '--train' in sys.argv
+if TRAIN:
+    from lib.density import image_bits_per_dim_graph  # noqa: E402
+    from lib.utils import ExponentialMovingAverage, update_lipschitz  # noqa: E402
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.99))
+    ema = ExponentialMovingAverage(model, decay=0.999)
+
+
 def step():
+    if TRAIN:
+        for p in params:
+            p.grad = None
+        bpd, _, _ = image_bits_per_dim_graph(model, x, arch['nvals'])
+        bpd.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.)
+        opt.step()
+        opt.zero_grad()
+        update_lipschitz(model)
+        ema.apply()
+        return bpd
     _, logpx, _ = image_logpx(model, x, arch['nvals'])
     s, n = dd.global_logpx_sum(logpx)
     return s
@@ -51,4 +73,4 @@ torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats('tottime').print_stats(25)
-st.sort_stats('cumtime').print_stats(40)
+st.sort_stats('cumtime').print_stats(60)
