@@ -504,10 +504,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         if (kn < nkt)
 #endif
         {
-          {
 #pragma unroll
           for (int m = 0; m < TM; ++m) ld3(m, min(kn, nkt - 1), ab[(d + D - 1) % D][m]);
-          }
         }
         if constexpr (BPIPE) {
 #if PB_SCHED
