@@ -49,8 +49,19 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 
 
 def mfma_mode():
-    """Arithmetic of the fused kernels, as inf_net_create picks it (INFLOW_MFMA=f32 selects exact fp32 MFMA)."""
-    return 'f32' if os.environ.get('INFLOW_MFMA', '').startswith('f') else 'bf16x6'
+    """Arithmetic of the fused kernels, as inf_net_create picks it (engine.hip: INFLOW_MFMA=f32 / bf16x6 / f16x3)."""
+    e = os.environ.get('INFLOW_MFMA', '')
+    return 'f32' if e.startswith('f3') else ('bf16x6' if e.startswith('b') else 'f16x3')
+
+
+MFMA_DESC = {
+    'bf16x6': 'bf16x6: fp32 operands split exactly into 3 bf16 pieces, 6 products per fp32 product, fp32 '
+              'accumulation (error at fp32 level, tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
+    'f16x3': 'f16x3: fp32 operands scaled by 2^s (weights per matrix; activations per pixel column in phases B/C, per '
+             'tile in phase A) and split into 2 fp16 pieces (|x - h - l| <= 2^-24 |x|), 3 products per fp32 product on '
+             'v_mfma_f32_32x32x16_f16, fp32 accumulation, exact unscale (error at fp32 level, '
+             'tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
+    'f32': 'f32: v_mfma_f32_32x32x2_f32'}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -186,8 +197,9 @@ def main():
     if torch.is_tensor(bpd):
         bpd = float(bpd)
     mm = mfma_mode()
-    fused_dom = 'net313' in _hip.tag_name(dom['tag'])
-    peak = X6_PEAK_TFLOPS if (mm == 'bf16x6' and fused_dom) else FP32_MFMA_PEAK_TFLOPS
+    # fp32-equivalent peak of the arithmetic the dominant kernel issues: its algorithmic FLOPs over the time its
+    # MFMA instructions take at their dense peak (engine prof peak_ms; frac = MFMA-pipe fraction)
+    peak = dom['flops'] / (dom['peak_ms'] * 1e9) if dom.get('peak_ms') else FP32_MFMA_PEAK_TFLOPS
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
         'samples/sec (whole node), %s training step (%s)' % (
@@ -196,9 +208,7 @@ def main():
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
-        'mfma': ('bf16x6: fp32 operands split exactly into 3 bf16 pieces, 6 products per fp32 product, fp32 '
-                 'accumulation (error at fp32 level, tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)'
-                 if mm == 'bf16x6' else 'f32: v_mfma_f32_32x32x2_f32'),
+        'mfma': MFMA_DESC[mm],
         'data': 'synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
                 % 'x'.join(map(str, arch['input_size'])),
         'config': {'workload': '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU'
@@ -209,9 +219,10 @@ def main():
         'bits_per_dim': round(bpd, 6),
         'roofline': {'bound': 'mfma', 'kernel': _hip.tag_name(dom['tag']), 'achieved': round(achieved, 2),
                      'peak': round(peak, 1), 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4),
-                     'peak_basis': ('fp32-equivalent: dense bf16 MFMA peak %.1f / 6 products' % BF16_MFMA_PEAK_TFLOPS
-                                    if peak != FP32_MFMA_PEAK_TFLOPS else 'dense fp32 MFMA peak'),
-                     'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not bf16 MFMA FLOPs',
+                     'peak_basis': ('fp32-equivalent: algorithmic FLOPs / time of the issued MFMA instructions at '
+                                    'their dense peak (bf16/f16 %.1f TF: 6 products per fp32 product in bf16x6 phases, '
+                                    '3 in f16x3 phases; f32 %.1f TF)' % (BF16_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS)),
+                     'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not MFMA instruction FLOPs',
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
                      'flops_per_launch': dom['flops'] / dom['launches']},
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),

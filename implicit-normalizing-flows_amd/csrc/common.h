@@ -61,6 +61,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
 // Block-wide sum (blockDim.x multiple of 64, <= 1024); result valid in every thread.
 template <typename T>
 __device__ __forceinline__ T block_sum(T v, T* scratch /* >= 16 */) {
@@ -122,6 +128,44 @@ __device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4& h, c
   c = mfma_bf16(a[0], m, c);
   c = mfma_bf16(a[1], h, c);
   c = mfma_bf16(a[0], h, c);
+  return c;
+}
+
+// ---- scaled two-piece fp16 ("h3") contraction: phase B of INF_MFMA_F16X3 (include/inflow.h) ----------
+// x*S = h + l + e with h = rne16(x*S), l = rne16(x*S - h) (x*S - h is exact in fp32), |e| <= 2^-24 |x*S|
+// while l stays a normal fp16, i.e. for |x*S| >= 2^-2.  S = 2^s puts a column's (or matrix's) max in
+// [2^14, 2^15): below max*2^-16 the pieces lose precision only in absolute terms <= max*2^-39.  Products
+// hh + hl + lh on v_mfma_f32_32x32x16_f16 (exact 22-bit products, fp32 accumulation); ll <= 2^-24 |x||w|.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// scale exponent s for a set whose max |x| is m: m * 2^s in [2^14, 2^15); 0 for m == 0 / inf / NaN
+__host__ __device__ __forceinline__ int h3_scale_exp(float m) {
+  if (!(m > 0.f) || !(m <= 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(m, &e);            // m = f 2^e, f in [0.5, 1)
+  const int s = 15 - e;
+  return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+__device__ __forceinline__ void split2h(const float (&x)[8], float S, u32x4& h, u32x4& l) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const _Float16 h0 = (_Float16)(x[2 * j] * S), h1 = (_Float16)(x[2 * j + 1] * S);   // v_cvt_pk_f16_f32 (rne)
+    const _Float16 l0 = (_Float16)__builtin_fmaf(x[2 * j], S, -(float)h0);             // exact, then rne
+    const _Float16 l1 = (_Float16)__builtin_fmaf(x[2 * j + 1], S, -(float)h1);
+    const f16x2 hv = {h0, h1}, lv = {l0, l1};
+    h[j] = __builtin_bit_cast(unsigned, hv);
+    l[j] = __builtin_bit_cast(unsigned, lv);
+  }
+}
+__device__ __forceinline__ f32x16 mfma_f16(const u32x4& a, const u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                0, 0, 0);
+}
+// acc += A.B with A = (h, l) planes of the scaled weights, B = (h, l) of the scaled activations; small first
+__device__ __forceinline__ f32x16 mfma_h3(const u32x4 (&a)[2], const u32x4& h, const u32x4& l, f32x16 c) {
+  c = mfma_f16(a[1], h, c);
+  c = mfma_f16(a[0], l, c);
+  c = mfma_f16(a[0], h, c);
   return c;
 }
 

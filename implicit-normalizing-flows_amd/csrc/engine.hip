@@ -30,19 +30,20 @@ void set_hip_error(hipError_t e) { g_last_hip = (int)e; }
 struct ProfSlot {
   hipEvent_t a, b;
   int tag;
-  double flops, bytes;
+  double flops, bytes, peak_ms;
 };
 static std::vector<ProfSlot> g_prof;
 static size_t g_prof_used = 0;
 static bool g_prof_on = false;
 bool prof_enabled() { return g_prof_on && g_prof_used < g_prof.size(); }
 void prof_begin_launch(hipStream_t s) { (void)hipEventRecord(g_prof[g_prof_used].a, s); }
-void prof_end_launch(hipStream_t s, int tag, double flops, double bytes) {
+void prof_end_launch(hipStream_t s, int tag, double flops, double bytes, double peak_ms) {
   ProfSlot& p = g_prof[g_prof_used++];
   (void)hipEventRecord(p.b, s);
   p.tag = tag;
   p.flops = flops;
   p.bytes = bytes;
+  p.peak_ms = peak_ms;
 }
 }  // namespace inf
 
@@ -93,6 +94,10 @@ struct InfNet {
   float *F1f = nullptr, *F1b = nullptr, *F2f = nullptr, *F2b = nullptr, *F3f = nullptr, *F3b = nullptr;
   // F1f..F3b split into three bf16 planes each (launch_split3), same order as F1f..F3b
   uint16_t* Fs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // F1f..F3b as two scaled fp16 planes each (launch_split2h, INF_MFMA_F16X3), same order as Fs; their scale
+  // exponents per direction: Fexp[3 * vjp + phase]
+  uint16_t* Fh[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int* Fexp = nullptr;
   int mfma_mode = INF_MFMA_F32;                 // InfMfmaMode of the fused kernel's phase B
   // f(0) of a conv net (the same image for every sample: zero input, zero padding), cached for the first
   // Broyden residual; computed by a launch of the same batch size (same tile variant -> same bits)
@@ -185,7 +190,7 @@ size_t ws_need(const InfNet* n, int B, int T) {
 GemmArgs gemm_base(const InfNet* n, const Operand& op, const float* X, int in_ch, int B) {
   GemmArgs g;
   memset(&g, 0, sizeof(g));
-  g.x6 = n->mfma_mode == INF_MFMA_BF16X6;
+  g.x6 = n->mfma_mode != INF_MFMA_F32;
   g.A = op.A;
   g.M = op.M;
   g.Kpad = op.Kpad;
@@ -223,10 +228,15 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.K1pad = n->K1pad;
   f.A2 = vjp ? n->F2b : n->F2f;
   f.A3 = vjp ? n->F3b : n->F3f;
-  const bool spl = n->mfma_mode == INF_MFMA_BF16X6;
+  const bool spl = n->mfma_mode != INF_MFMA_F32;
+  const bool h3 = n->mfma_mode == INF_MFMA_F16X3;
   f.A1s = spl ? (const void*)n->Fs[vjp ? 1 : 0] : nullptr;
   f.A2s = spl ? (const void*)n->Fs[vjp ? 3 : 2] : nullptr;
   f.A3s = spl ? (const void*)n->Fs[vjp ? 5 : 4] : nullptr;
+  f.A1h = h3 ? (const void*)n->Fh[vjp ? 1 : 0] : nullptr;
+  f.A2h = h3 ? (const void*)n->Fh[vjp ? 3 : 2] : nullptr;
+  f.A3h = h3 ? (const void*)n->Fh[vjp ? 5 : 4] : nullptr;
+  f.Ah_exp = h3 ? n->Fexp + (vjp ? 3 : 0) : nullptr;
   f.M3 = n->M3;
   f.M3pad = n->M3pad;
   f.b1 = n->L[0].b;
@@ -1041,9 +1051,12 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
       // split planes: 3 bf16 (= 1.5 floats) per element of each of the six operands
       floats += 3 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
+      // F16X3 planes: 2 fp16 (= 1 float) per element of each of the six operands, plus the scale exponents
+      floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64 + 64;
       n->rows_max = std::max(n->rows_max, n->M3);
-      const char* mm = getenv("INFLOW_MFMA");             // "f32" / "bf16x6" (default)
-      n->mfma_mode = (mm && mm[0] == 'f') ? INF_MFMA_F32 : INF_MFMA_BF16X6;
+      const char* mm = getenv("INFLOW_MFMA");             // "f32" / "bf16x6" / "f16x3" (default)
+      n->mfma_mode = (mm && mm[0] == 'f' && mm[1] == '3') ? INF_MFMA_F32
+                     : (mm && mm[0] == 'b') ? INF_MFMA_BF16X6 : INF_MFMA_F16X3;
     }
   }
   // sigma scratch: one partial per 256 output elements of the largest conv (or per channel-split block)
@@ -1078,13 +1091,19 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       n->Fs[i] = reinterpret_cast<uint16_t*>(p);
       p += (3 * sz[i] + 1) / 2 + 64;
     }
+    for (int i = 0; i < 6; ++i) {
+      n->Fh[i] = reinterpret_cast<uint16_t*>(p);
+      p += sz[i] + 64;
+    }
+    n->Fexp = reinterpret_cast<int*>(p);
+    p += 64;
   }
   *out = n;
   return INF_OK;
 }
 
 int inf_net_set_mfma(InfNet* n, int mode) {
-  if (!n || (mode != INF_MFMA_F32 && mode != INF_MFMA_BF16X6)) return INF_ERR_INVALID;
+  if (!n || (mode != INF_MFMA_F32 && mode != INF_MFMA_BF16X6 && mode != INF_MFMA_F16X3)) return INF_ERR_INVALID;
   n->mfma_mode = mode;
   return INF_OK;
 }
@@ -1123,6 +1142,7 @@ int inf_net_refresh(InfNet* n, void* stream) {
     const long cnt[6] = {(long)H * n->K1pad, (long)H * n->K1pad, (long)H * H, (long)H * H, (long)n->M3pad * H,
                          (long)n->M3pad * H};
     for (int i = 0; i < 6; ++i) INF_TRY(launch_split3(src[i], n->Fs[i], cnt[i], s));
+    for (int i = 0; i < 6; ++i) INF_TRY(launch_split2h(src[i], n->Fh[i], cnt[i], n->Fexp + 3 * (i & 1) + i / 2, s));
   }
   return INF_OK;
 }
@@ -1742,6 +1762,7 @@ int inf_profile_end(InfKernelStat* out, int max_out, int* n_out) {
     st->total_ms += ms;
     st->flops += p.flops;
     st->bytes += p.bytes;
+    st->peak_ms += p.peak_ms;
   }
   const int n = (int)std::min<size_t>(agg.size(), (size_t)std::max(max_out, 0));
   for (int i = 0; i < n; ++i) out[i] = agg[i];

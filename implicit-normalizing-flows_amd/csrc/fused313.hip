@@ -64,14 +64,42 @@ __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = v1.w;
 }
 
+// Split operands, generic over the plane count NP: 3 = exact bf16 split (x6), 2 = scaled fp16 split (h3).
+// Weight planes: fragment tile `tile` holds NP planes of 64 lanes x 8 values, plane p at u32x4 offset
+// (tile * NP + p) * 64 + lane (launch_split3 / launch_split2h).
+template <int NP>
+__device__ __forceinline__ void ldw(const u32x4* base, long tile, int lane, u32x4 (&o)[NP]) {
+  const u32x4* q = base + tile * NP * 64 + lane;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) o[p] = q[64 * p];
+}
+template <int NP>
+__device__ __forceinline__ void splitb(const float (&x)[8], float S, u32x4 (&o)[NP]) {
+  if constexpr (NP == 3) split3(x, o[0], o[1], o[2]);
+  else split2h(x, S, o[0], o[1]);
+}
+template <int NP>
+__device__ __forceinline__ f32x16 mma(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16 c) {
+  if constexpr (NP == 3) return mfma_x6(a, b[0], b[1], b[2], c);
+  else return mfma_h3(a, b[0], b[1], c);
+}
+#ifndef H3_AC
+#define H3_AC 1      // INF_MFMA_F16X3: phases A and C in h3 too (0: x6 there)
+#endif
+
 // fragment-major offset of (row block rb, k tile kt) for a matrix with nkt K tiles
 __device__ __forceinline__ long frag_off(int rb, int kt, int nkt, int lane) {
   return (((long)rb * nkt + kt) * 64 + lane) * 8;
 }
 
+// SPL: 0 exact fp32 MFMA, 1 split-bf16 (x6) in all phases, 2 x6 in phases A / C and the scaled fp16 split
+// (h3, common.h) in phase B (INF_MFMA_F16X3)
 template <int TM, int MODE, int F_BN, int F_LDS_FLOATS, int SPL = 0, int NW = 8>
 __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   constexpr int NT = 64 * NW;                        // threads per workgroup
+  constexpr bool H3 = SPL == 2;
+  constexpr bool H3AC = H3 && H3_AC;                  // phases A and C in h3 as well
+  constexpr int NPAC = H3AC ? 2 : 3;                  // weight / operand planes of phases A and C
   constexpr int HID = NW * 32 * TM;
   constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
   // two independent nets (the x- and z-branch of an imBlock) can share one launch
@@ -116,19 +144,16 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // split path: phase A's first operand tile is requested before the staging loads (it is an L2 hit and
   // retires long before the staging data, so it costs the staging nothing and phase A starts without a wait)
   const int rbw0 = wid * TM;
-  u32x4 pa0[TM][3];
+  u32x4 pa0[TM][NPAC];
   constexpr bool PRE_A = SPL && F_LDS_FLOATS != LDS_HALF;   // (not in the 128-VGPR variant)
+  const u32x4* A1w = reinterpret_cast<const u32x4*>(H3AC ? a.A1h : a.A1s);
+  const u32x4* A3w = reinterpret_cast<const u32x4*>(H3AC ? a.A3h : a.A3s);
   if constexpr (PRE_A) {
-    const u32x4* A1s = reinterpret_cast<const u32x4*>(a.A1s);
     const int nkt1 = a.K1pad / 16;
 #pragma unroll
-    for (int m = 0; m < TM; ++m) {
-      const u32x4* q = A1s + ((long)((rbw0 + m) * nkt1) * 3) * 64 + lane;
-      pa0[m][0] = q[0];
-      pa0[m][1] = q[64];
-      pa0[m][2] = q[128];
-    }
+    for (int m = 0; m < TM; ++m) ldw<NPAC>(A1w, (long)(rbw0 + m) * nkt1, lane, pa0[m]);
   }
+  float hmx = 0.f;                                  // H3AC: this thread's max |staged halo value|
   // ---- stage the input halo tile (zero padded; forward applies the preact swish) ----
   // Series chaining: the input is the previous VJP's packed taps; the tap sum, the preact swish'
   // multiplier and that term's trace partial (conv_out's OM_VJP work) happen here instead.
@@ -190,6 +215,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         v = ok ? v : 0.f;
         if (ep && ok == 2) dacc += (double)v * (double)ev[u];
         if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
+        if constexpr (H3AC) hmx = fmaxf(hmx, fabsf(v));
         if (i < vhz) vh[i] = v;
       }
     };
@@ -213,11 +239,20 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           if (a.pre_beta) v = swish_f(v, pre_sp);
         }
       }
+      if constexpr (H3AC) hmx = fmaxf(hmx, fabsf(v));
       vh[i] = v;
     }
   }
   // per-tile trace partial: wave sums -> a reserved LDS slot at the end of the LDS (never reused)
   double* red = reinterpret_cast<double*>(smem + F_LDS_FLOATS - 16);
+  // H3: per-wave column maxima of the phase-B / phase-C operand [NW][F_BN] and the halo maxima [NW] of
+  // phase A, just below the trace-partial slots
+  float* cmax = smem + F_LDS_FLOATS - 16 - 16 - NW * F_BN;
+  float* hmax = smem + F_LDS_FLOATS - 32;
+  if constexpr (H3AC) {
+    const float w = wave_max(hmx);
+    if (lane == 0) hmax[wid] = w;
+  }
   if (a.dot_part) {
     const double w = wave_sum(dacc);
     if (lane == 0) red[wid] = w;
@@ -306,13 +341,18 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   zero_acc();
   if constexpr (SPL) {
     const int nkt = a.K1pad / 16;
-    const u32x4* A1s = reinterpret_cast<const u32x4*>(a.A1s);
-    auto ld3 = [&](int m, int kt, u32x4 (&o)[3]) {
-      const u32x4* q = A1s + ((long)((rbw + m) * nkt + kt) * 3) * 64 + lane;
-      o[0] = q[0];
-      o[1] = q[64];
-      o[2] = q[128];
-    };
+    // H3AC: one scale for the tile's halo (its max over all waves), unscaled after the K loop
+    float sA = 1.f;
+    int eA = 0;
+    if constexpr (H3AC) {
+      float m_ = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m_ = fmaxf(m_, hmax[w]);
+      const int sc = h3_scale_exp(m_);
+      sA = __builtin_amdgcn_ldexpf(1.f, sc);
+      eA = -(sc + a.Ah_exp[0]);
+    }
+    auto ld3 = [&](int m, int kt, u32x4 (&o)[NPAC]) { ldw<NPAC>(A1w, (long)(rbw + m) * nkt + kt, lane, o); };
     // B operand (im2col gather from the halo tile) one K tile ahead: its LDS reads and split overlap
     // this tile's MFMAs
     auto gath = [&](int kt, float (&x)[NB][8]) {
@@ -326,37 +366,37 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int kk = 0; kk < 8; ++kk) x[b][kk] = vh[ko[kk] + pix[b]];
     };
     // (the 128-VGPR variant gathers and splits in place)
-    u32x4 bh[NB], bm[NB], bl[NB];
+    u32x4 bq[NB][NPAC];
     if constexpr (PRE_A) {
       float x0[NB][8];
       gath(0, x0);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) split3(x0[b], bh[b], bm[b], bl[b]);
+      for (int b = 0; b < NB; ++b) splitb<NPAC>(x0[b], sA, bq[b]);
     }
-    auto tileA = [&](int kt, const u32x4 (&af)[TM][3]) {
+    auto tileA = [&](int kt, const u32x4 (&af)[TM][NPAC]) {
       float xn[NB][8];
       if constexpr (PRE_A) {
         gath(min(kt + 1, nkt - 1), xn);
       } else {
         gath(kt, xn);
 #pragma unroll
-        for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+        for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
       }
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_x6(af[m], bh[b], bm[b], bl[b], acc[m][b]);
+        for (int b = 0; b < NB; ++b) acc[m][b] = mma<NPAC>(af[m], bq[b], acc[m][b]);
       if constexpr (PRE_A) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) split3(xn[b], bh[b], bm[b], bl[b]);
+        for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
       }
     };
-    u32x4 a0[TM][3], a1[TM][3];
+    u32x4 a0[TM][NPAC], a1[TM][NPAC];
 #pragma unroll
     for (int m = 0; m < TM; ++m) {
       if constexpr (PRE_A) {
 #pragma unroll
-        for (int p3 = 0; p3 < 3; ++p3) a0[m][p3] = pa0[m][p3];
+        for (int p3 = 0; p3 < NPAC; ++p3) a0[m][p3] = pa0[m][p3];
       } else {
         ld3(m, 0, a0[m]);
       }
@@ -373,6 +413,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
       }
       if (has1) tileA(kt + 1, a1);
+    }
+    if constexpr (H3AC) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], eA);
     }
   } else {
     const int nkt = a.K1pad / 16;
@@ -415,6 +463,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // epilogue A -> t (LDS); SAVE: d1 -> HBM
   {
     const float sp1 = (MODE != MODE_VJP) ? softplus_f(*a.beta1) : 0.f;
+    float cm[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) cm[b] = 0.f;
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -431,17 +482,101 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             v = swish_f(z, sp1);
             if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) dv[r] = swish_d(z, sp1);
           }
+          if constexpr (H3) cm[b] = fmaxf(cm[b], fabsf(v));
           t[o * F_BN + b * 32 + li] = v;
         }
         if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) store_d(a.d1, m, b, dv);
       }
+    if constexpr (H3) {
+      // column n = 32 b + li: lanes li and li + 32 hold different rows of it
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        cm[b] = fmaxf(cm[b], __shfl_xor(cm[b], 32, 64));
+        if (lh == 0) cmax[wid * F_BN + b * 32 + li] = cm[b];
+      }
+    }
   }
   __syncthreads();
   STAMP(3);
 
   // ---------------------------------------------------------------- phase B: K = HID (from LDS)
   zero_acc();
-  if constexpr (SPL) {
+  int hexp[NB];                                      // H3: unscale exponent per pixel column
+  if constexpr (H3) {
+    constexpr int nkt = HID / 16;
+    const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);   // (phase-B planes: a.A2h)
+    const int sw = a.Ah_exp[1];
+    float hs[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float m_ = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m_ = fmaxf(m_, cmax[w * F_BN + b * 32 + li]);
+      const int sc = h3_scale_exp(m_);
+      hs[b] = __builtin_amdgcn_ldexpf(1.f, sc);
+      hexp[b] = -(sc + sw);
+    }
+    auto ld2 = [&](int m, int kt, u32x4 (&o)[2]) {
+      const u32x4* q = A2h + ((long)((rbw + m) * nkt + kt) * 2) * 64 + lane;
+      o[0] = q[0];
+      o[1] = q[64];
+    };
+    struct BOpH { u32x4 h[NB], l[NB]; };
+    auto bprep = [&](int kt, BOpH& o) {
+      const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float x[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x[kk] = tb[kk * F_BN + 32 * b];
+        split2h(x, hs[b], o.h[b], o.l[b]);
+      }
+    };
+    auto bmma = [&](const u32x4 (&af)[TM][2], const BOpH& o) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[m][b] = mfma_h3(af[m], o.h[b], o.l[b], acc[m][b]);
+    };
+    constexpr int D = 2;
+    constexpr bool BPIPE = PB_BPIPE && F_LDS_FLOATS != LDS_HALF;
+    u32x4 ab[D][TM][2];
+    BOpH bo[BPIPE ? 2 : 1];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ld2(m, 0, ab[0][m]);
+    if constexpr (BPIPE) bprep(0, bo[0]);
+    for (int kt = 0; kt < nkt; kt += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int kn = kt + d + D - 1;
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ld2(m, min(kn, nkt - 1), ab[(d + D - 1) % D][m]);
+        if constexpr (BPIPE) {
+          bprep(min(kt + d + 1, nkt - 1), bo[(d + 1) % 2]);
+          bmma(ab[d], bo[d % 2]);
+#if PB_SCHED
+          __builtin_amdgcn_sched_group_barrier(0x020, TM * 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 * NB, 0);
+#pragma unroll
+          for (int i = 0; i < 3 * TM * NB - 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, PB_SCHED, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#endif
+        } else {
+          bprep(kt + d, bo[0]);
+          bmma(ab[d], bo[0]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], hexp[b]);
+  } else if constexpr (SPL) {
     constexpr int nkt = HID / 16;
     const u32x4* A2s = reinterpret_cast<const u32x4*>(a.A2s);
     auto ld3 = [&](int m, int kt, u32x4 (&o)[3]) {
@@ -624,8 +759,31 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
+    if constexpr (H3AC) {
+      // phase C's per-column scales (cmax is free again: every wave read it before phase B, i.e. before the
+      // barrier above)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float c_ = 0.f;
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) c_ = fmaxf(c_, fabsf(acc[m][b][r]));
+        c_ = fmaxf(c_, __shfl_xor(c_, 32, 64));
+        if (lh == 0) cmax[wid * F_BN + b * 32 + li] = c_;
+      }
+    }
     __syncthreads();
     STAMP(5);
+    // H3AC: scale of this lane's column b, and the unscale exponent of its phase-C results
+    auto colscale = [&](int b, float& S, int& e) {
+      float m_ = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m_ = fmaxf(m_, cmax[w * F_BN + b * 32 + li]);
+      const int sc = h3_scale_exp(m_);
+      S = __builtin_amdgcn_ldexpf(1.f, sc);
+      e = -(sc + a.Ah_exp[2]);
+    };
 
     // -------------------------------------------------------------- phase C: taps, K = HID
     // tasks = (32-row block of the M3pad tap rows) x (32-pixel column); split K when there are
@@ -650,22 +808,11 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
     if constexpr (SPL) {
-      const u32x4* A3s = reinterpret_cast<const u32x4*>(a.A3s);
-      auto ld3 = [&](int rb, int kt, u32x4 (&o)[3]) {
-        const u32x4* q = A3s + ((long)(rb * nkt + kt) * 3) * 64 + lane;
-        o[0] = q[0];
-        o[1] = q[64];
-        o[2] = q[128];
-      };
+      auto ld3 = [&](int rb, int kt, u32x4 (&o)[NPAC]) { ldw<NPAC>(A3w, (long)rb * nkt + kt, lane, o); };
       auto bread = [&](int b, int kt, float (&x)[8]) {
         const float* tc = t + (kt * 16 + lh * 8) * F_BN + b * 32 + li;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) x[kk] = tc[kk * F_BN];
-      };
-      auto bsplit = [&](int b, int kt, u32x4& h, u32x4& m, u32x4& l) {
-        float x[8];
-        bread(b, kt, x);
-        split3(x, h, m, l);
       };
       if (ksplit > 1 || njobs - jbase <= NW) {
         // at most one job per wave: one K chain of 6 MFMAs per K tile, so the operand stream is
@@ -675,22 +822,30 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           const int task = job / ksplit, ks = job - task * ksplit;
           const int rb = task / NB, b = task % NB;
           const int k_lo = ks * kts, k_hi = (ks + 1) * kts;     // kts is even
+          float sC = 1.f;
+          int eC = 0;
+          if constexpr (H3AC) colscale(b, sC, eC);
+          auto bsplit = [&](int kt, u32x4 (&o)[NPAC]) {
+            float x[8];
+            bread(b, kt, x);
+            splitb<NPAC>(x, sC, o);
+          };
           // B operand one K tile ahead: its LDS reads and split overlap this tile's MFMA chain
-          u32x4 h, m, l;
-          if constexpr (PRE_A) bsplit(b, k_lo, h, m, l);
-          auto step = [&](int kt, const u32x4 (&af)[3]) {
+          u32x4 bq[NPAC];
+          if constexpr (PRE_A) bsplit(k_lo, bq);
+          auto step = [&](int kt, const u32x4 (&af)[NPAC]) {
             if constexpr (PRE_A) {
               float xn[8];
               bread(b, min(kt + 1, k_hi - 1), xn);
-              cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
-              split3(xn, h, m, l);
+              cacc[0] = mma<NPAC>(af, bq, cacc[0]);
+              splitb<NPAC>(xn, sC, bq);
             } else {
-              bsplit(b, kt, h, m, l);
-              cacc[0] = mfma_x6(af, h, m, l, cacc[0]);
+              bsplit(kt, bq);
+              cacc[0] = mma<NPAC>(af, bq, cacc[0]);
             }
           };
           if (F_LDS_FLOATS != LDS_HALF && (k_hi - k_lo) % 4 == 0) {   // (HID 256 with ksplit 8: 2 K tiles)
-            u32x4 r0[3], r1[3], r2[3], r3[3];
+            u32x4 r0[NPAC], r1[NPAC], r2[NPAC], r3[NPAC];
             ld3(rb, k_lo, r0);
             ld3(rb, k_lo + 1, r1);
             ld3(rb, k_lo + 2, r2);
@@ -705,7 +860,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
               step(kt + 3, r3);
             }
           } else {   // 128-VGPR variant, or a K range that is not a multiple of 4 tiles: ping-pong
-            u32x4 r0[3], r1[3];
+            u32x4 r0[NPAC], r1[NPAC];
             ld3(rb, k_lo, r0);
             for (int kt = k_lo; kt < k_hi; kt += 2) {
               ld3(rb, kt + 1, r1);
@@ -714,6 +869,10 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
               step(kt + 1, r1);
             }
           }
+          if constexpr (H3AC) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cacc[0][r] = __builtin_amdgcn_ldexpf(cacc[0][r], eC);
+          }
         }
       } else {
         // ksplit == 1 and several jobs per wave: a wave's jobs share its pixel column (NW % NB == 0),
@@ -721,6 +880,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         // (groups of G = 2 jobs; G = 1 in the 128-VGPR variant)
         constexpr int G = (F_LDS_FLOATS == LDS_HALF) ? 1 : 2;
         const int b = (jbase + wid) % NB;
+        float sC = 1.f;
+        int eC = 0;
+        if constexpr (H3AC) colscale(b, sC, eC);
+        auto bsplit = [&](int kt, u32x4 (&o)[NPAC]) {
+          float x[8];
+          bread(b, kt, x);
+          splitb<NPAC>(x, sC, o);
+        };
 #pragma unroll
         for (int jp = 0; jp < 4 / G; ++jp) {
           const int job0 = jbase + wid + NW * (G * jp);
@@ -733,28 +900,34 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             vj[g] = job < njobs;
             rbj[g] = vj[g] ? job / NB : job0 / NB;
           }
-          u32x4 h, m, l;
-          if constexpr (PRE_A) bsplit(b, 0, h, m, l);
-          auto step = [&](int kt, const u32x4 (&af)[G][3]) {
+          u32x4 bq[NPAC];
+          if constexpr (PRE_A) bsplit(0, bq);
+          auto step = [&](int kt, const u32x4 (&af)[G][NPAC]) {
             float xn[8];
             if constexpr (PRE_A) bread(b, min(kt + 1, nkt - 1), xn);
-            else bsplit(b, kt, h, m, l);
+            else bsplit(kt, bq);
 #pragma unroll
             for (int g = 0; g < G; ++g)
-              if (vj[g]) cacc[G * jp + g] = mfma_x6(af[g], h, m, l, cacc[G * jp + g]);
-            if constexpr (PRE_A) split3(xn, h, m, l);
+              if (vj[g]) cacc[G * jp + g] = mma<NPAC>(af[g], bq, cacc[G * jp + g]);
+            if constexpr (PRE_A) splitb<NPAC>(xn, sC, bq);
           };
-          auto ldg = [&](int kt, u32x4 (&o)[G][3]) {
+          auto ldg = [&](int kt, u32x4 (&o)[G][NPAC]) {
 #pragma unroll
             for (int g = 0; g < G; ++g) ld3(rbj[g], kt, o[g]);
           };
-          u32x4 p0[G][3], q0[G][3];
+          u32x4 p0[G][NPAC], q0[G][NPAC];
           ldg(0, p0);
           for (int kt = 0; kt < nkt; kt += 2) {
             ldg(kt + 1, q0);
             step(kt, p0);
             if (kt + 2 < nkt) ldg(kt + 2, p0);
             step(kt + 1, q0);
+          }
+          if constexpr (H3AC) {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) cacc[G * jp + g][r] = __builtin_amdgcn_ldexpf(cacc[G * jp + g][r], eC);
           }
         }
       }
@@ -857,7 +1030,7 @@ static int tile_fits(int hid, int C, int H, int W, int bn, int ldsf) {
   const int rows = bn / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
   const long need = (long)hid * bn + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
-  return need <= ldsf - 16;                                // last 16 floats: trace-partial slots
+  return need <= ldsf - 32 - 8 * bn;       // last 16 floats: trace-partial slots; 16 + 8 x bn: H3 halo / column maxima
 }
 static int variant_fits(int hid, int C, int H, int W, int v) {
   if (v == V64) return tile_fits(hid, C, H, W, 64, LDS_FULL);
@@ -996,6 +1169,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     return e ? atoi(e) : 1;
   }();
   const bool split = pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr && (var != VHALF || split_h);
+  const bool h3 = split && pr.a[0].A1h != nullptr && pr.a[1].A1h != nullptr;
   static const int quad_env = [] {
     const char* e = getenv("INFLOW_FUSED_NW");            // tuning knob: 4 = one wave per SIMD (64-px tiles)
     return e ? atoi(e) : 8;
@@ -1005,14 +1179,15 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   if (prof) prof_begin_launch(s);
 #define L313S(TM_, MODE_, SPL_)                                                                         \
   do {                                                                                                  \
-    if (var == V64 && quad) hipLaunchKernelGGL((net313_kernel_q<TM_, MODE_, SPL_>), dim3(nb), dim3(256), 0, s, pr); \
+    if (var == V64 && quad && SPL_ < 2) hipLaunchKernelGGL((net313_kernel_q<TM_, MODE_, (SPL_ < 2 ? SPL_ : 1)>), dim3(nb), dim3(256), 0, s, pr); \
     else if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
     else if (var == VHALF) hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
     else hipLaunchKernelGGL((net313_kernel_w<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr);           \
   } while (0)
 #define L313(TM_, MODE_, BN_)            \
   do {                                   \
-    if (split) L313S(TM_, MODE_, 1);     \
+    if (h3) L313S(TM_, MODE_, 2);        \
+    else if (split) L313S(TM_, MODE_, 1); \
     else L313S(TM_, MODE_, 0);           \
   } while (0)
 #define L313M(TM_, BN_)                                \
@@ -1030,7 +1205,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   INF_CHECK_LAUNCH();
   if (pr.tbuf) {
     char key[64];
-    snprintf(key, sizeof(key), "var%d mode%d split%d C%d", var, mode, (int)split, a0.C);
+    snprintf(key, sizeof(key), "var%d mode%d split%d C%d", var, mode, (int)split + (int)h3, a0.C);
     timing_collect(key, (long)nb, s);
   }
   if (prof) {
@@ -1039,7 +1214,10 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
     const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
     // (EVALSAVE: x + d1/d2 writes + taps, the same expression)
-    prof_end_launch(s, 500 + 10 * var + mode, npx * (fA + fB + fC), bytes);   // 50x / 51x (_h) / 52x (_w)
+    // MFMA instruction FLOPs: exact fp32 1 per algorithmic FLOP (f32 peak), x6 6 (bf16), h3 phase B 3 (f16)
+    const double pk = !split ? npx * (fA + fB + fC) / PEAK_F32_FLOPS_PER_MS
+                             : npx * ((h3 && H3_AC ? 3.0 : 6.0) * (fA + fC) + (h3 ? 3.0 : 6.0) * fB) / PEAK_BF16_FLOPS_PER_MS;
+    prof_end_launch(s, 500 + 10 * var + mode, npx * (fA + fB + fC), bytes, pk);   // 50x / 51x (_h) / 52x (_w)
   }
   return INF_OK;
 }

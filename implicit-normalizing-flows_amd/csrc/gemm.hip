@@ -376,7 +376,8 @@ static int run(const GemmArgs& g, hipStream_t s) {
     const double flops = 2.0 * g.M * (double)g.N * g.Ktot;
     const bool dio = EPI == EP_MUL_DERIV || ((EPI >= EP_ACT_SWISH) && g.deriv_out);
     const double bytes = 4.0 * ((double)g.M * g.Ktot + (double)g.Ktot * g.N + (double)g.M * g.N * (1 + (dio ? 1 : 0)));
-    prof_end_launch(s, tag, flops, bytes);
+    prof_end_launch(s, tag, flops, bytes,
+                    g.x6 ? 6.0 * flops / PEAK_BF16_FLOPS_PER_MS : flops / PEAK_F32_FLOPS_PER_MS);
   }
   return INF_OK;
 }

@@ -482,7 +482,8 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
     INF_CHECK_LAUNCH();
     if (prof) {
       const double K = (double)a.B * a.P;
-      prof_end_launch(s, 800 + 10 * tmw + tnw, 2.0 * a.M * a.N * K, 4.0 * K * (a.M + (double)a.N / (a.ks * a.ks)));
+      prof_end_launch(s, 800 + 10 * tmw + tnw, 2.0 * a.M * a.N * K, 4.0 * K * (a.M + (double)a.N / (a.ks * a.ks)),
+                      2.0 * a.M * a.N * K / PEAK_F32_FLOPS_PER_MS);
     }
     const long n = (long)a.M * a.N;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.slab, nsplit, n,

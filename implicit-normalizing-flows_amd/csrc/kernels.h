@@ -107,6 +107,9 @@ int launch_pack(const float* W, const float* factor, float* dst, int cout, int c
 // Split a fragment-major fp32 operand (n = Mpad * Kpad floats) into three bf16 planes per 512-float
 // fragment tile: dst[(tile * 3 + plane) * 512 + w] (fused313.hip split phase B).
 int launch_split3(const float* src, uint16_t* dst, long n, hipStream_t s);
+// Scale exponent of a whole operand (*exp_out = h3_scale_exp(max |src|), common.h) and its two scaled fp16
+// planes per 512-float fragment tile: dst[(tile * 2 + plane) * 512 + w] (fused313.hip phase B, F16X3).
+int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStream_t s);
 
 // exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
@@ -139,6 +142,12 @@ struct Net313Args {
   const void* A1s;
   const void* A2s;
   const void* A3s;
+  // A1h / A2h / A3h: the operands as two scaled fp16 planes (h, l) per fragment tile, scales 2^Ah_exp[0..2]
+  // (common.h split2h); non-null (with A1s..A3s) selects INF_MFMA_F16X3 (h3 in phase B, and in A / C with H3_AC)
+  const void* A1h;
+  const void* A2h;
+  const void* A3h;
+  const int* Ah_exp;
   int M3, M3pad;          // 9C taps rows
   const float* b1;
   const float* beta1;
@@ -207,6 +216,9 @@ int launch_sigma_chain(const float* dWe, const float* W, const float* dsig, cons
 // ------------------------------------------------------------------------------------------
 bool prof_enabled();
 void prof_begin_launch(hipStream_t s);
-void prof_end_launch(hipStream_t s, int tag, double flops, double bytes);
+// peak_ms: the launch's MFMA instruction FLOPs at the dense peak of their type (0: not an MFMA kernel)
+void prof_end_launch(hipStream_t s, int tag, double flops, double bytes, double peak_ms = 0.0);
+constexpr double PEAK_F32_FLOPS_PER_MS = 157.3e9;      // MI355X_MICROARCH.md dense fp32 matrix peak
+constexpr double PEAK_BF16_FLOPS_PER_MS = 2516.6e9;    // dense bf16 / f16 MFMA peak
 
 }  // namespace inf

@@ -608,6 +608,40 @@ int launch_split3(const float* src, uint16_t* dst, long n, hipStream_t s) {
   return INF_OK;
 }
 
+// One workgroup: *exp_out = h3_scale_exp(max |src|) over the whole operand.
+__global__ __launch_bounds__(1024) void amax_exp_kernel(const float* src, long n, int* exp_out) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (long i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(src[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    for (int w = 0; w < 16; ++w) r = fmaxf(r, red[w]);
+    *exp_out = h3_scale_exp(r);
+  }
+}
+// Two scaled fp16 pieces per element (common.h split2h): h = rne16(x 2^s), l = rne16(x 2^s - h).
+__global__ void split2h_kernel(const float* src, uint16_t* dst, long n, const int* exp) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float S = ldexpf(1.f, *exp);
+  const float x = src[i];
+  const _Float16 h = (_Float16)(x * S);
+  const _Float16 l = (_Float16)__builtin_fmaf(x, S, -(float)h);
+  const long tile = i >> 9, w = i & 511;
+  dst[(tile * 2 + 0) * 512 + w] = __builtin_bit_cast(uint16_t, h);
+  dst[(tile * 2 + 1) * 512 + w] = __builtin_bit_cast(uint16_t, l);
+}
+int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStream_t s) {
+  hipLaunchKernelGGL(amax_exp_kernel, dim3(1), dim3(1024), 0, s, src, n, exp_out);
+  hipLaunchKernelGGL(split2h_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, (const int*)exp_out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // exact log|det(I + T)| per sample (torch.logdet via LU, implicit_block.py:253-258).  T is stored
 // feature-major as tangents: T[i][j] of sample b at tang[i * ld + (j + 1) * stride_j + b],

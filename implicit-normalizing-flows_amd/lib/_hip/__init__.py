@@ -56,7 +56,7 @@ class BroydenStats(ctypes.Structure):
 
 class KernelStat(ctypes.Structure):
     _fields_ = [('tag', ctypes.c_int), ('launches', ctypes.c_int), ('total_ms', ctypes.c_double),
-                ('flops', ctypes.c_double), ('bytes', ctypes.c_double)]
+                ('flops', ctypes.c_double), ('bytes', ctypes.c_double), ('peak_ms', ctypes.c_double)]
 
 
 class HipError(RuntimeError):
@@ -322,7 +322,7 @@ def profile_end():
     n = ctypes.c_int()
     check(load().inf_profile_end(arr, 256, ctypes.byref(n)), 'inf_profile_end')
     return [dict(tag=arr[i].tag, launches=arr[i].launches, total_ms=arr[i].total_ms, flops=arr[i].flops,
-                 bytes=arr[i].bytes) for i in range(min(n.value, 256))]
+                 bytes=arr[i].bytes, peak_ms=arr[i].peak_ms) for i in range(min(n.value, 256))]
 
 
 def tag_name(tag):

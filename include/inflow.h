@@ -87,9 +87,15 @@ int inf_net_refresh(InfNet* net, void* stream);
  *   INF_MFMA_BF16X6 both operands split exactly into three bf16 pieces (x = hi + mid + lo, truncation),
  *                   the six products down to 2^-16 relative on v_mfma_f32_32x32x16_bf16, fp32 accumulation:
  *                   dropped terms <= 2^-23 relative, i.e. fp32-level error at 16x the per-clock MFMA rate.
- * Default: INFLOW_MFMA=f32 in the environment at inf_net_create selects F32, otherwise BF16X6.
+ *   INF_MFMA_F16X3  phases A and C as BF16X6; phase B (the HID x HID contraction) with both operands split
+ *                   into two fp16 pieces after a power-of-two scale (weights: per matrix; activations: per
+ *                   pixel column, from the column's max), x*S = h + l with h = rne16(x*S), l = rne16(x*S - h):
+ *                   |x*S - h - l| <= 2^-24 |x*S|; three products (lh, hl, hh) on v_mfma_f32_32x32x16_f16,
+ *                   fp32 accumulation, unscaled exactly (ldexp) in the epilogue: fp32-level error at
+ *                   twice the BF16X6 product rate, 4 instead of 6 operand bytes per weight.
+ * Default: INFLOW_MFMA=f32 / bf16x6 / f16x3 in the environment at inf_net_create, otherwise F16X3.
  * No effect on nets outside the fused path. */
-typedef enum InfMfmaMode { INF_MFMA_F32 = 0, INF_MFMA_BF16X6 = 1 } InfMfmaMode;
+typedef enum InfMfmaMode { INF_MFMA_F32 = 0, INF_MFMA_BF16X6 = 1, INF_MFMA_F16X3 = 2 } InfMfmaMode;
 int inf_net_set_mfma(InfNet* net, int mode);
 int inf_net_get_mfma(const InfNet* net);
 /* Workspace for any call below on a net of this shape at this batch size. */
@@ -193,6 +199,9 @@ typedef struct InfKernelStat {
   double total_ms;  /* sum of event-measured launch durations */
   double flops;     /* algorithmic FLOPs of those launches */
   double bytes;     /* algorithmic bytes of those launches */
+  double peak_ms;   /* time those launches' MFMA instructions take at the dense matrix peak of their type
+                       (f32 157.3 TF; bf16 / f16 2516.6 TF, MI355X_MICROARCH.md): peak_ms / total_ms is the
+                       MFMA-pipe fraction, flops / peak_ms the fp32-equivalent peak of the arithmetic used */
 } InfKernelStat;
 int inf_profile_begin(int max_launches);
 int inf_profile_end(InfKernelStat* out, int max_out, int* n_out);

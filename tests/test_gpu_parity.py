@@ -234,7 +234,7 @@ def test_device_rademacher():
     assert abs(p.mean().item()) < 0.01
 
 
-@pytest.mark.parametrize('mfma', [0, 1])
+@pytest.mark.parametrize('mfma', [0, 1, 2])
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3, 5])
 def test_fused_313_matches_generic_path(block, B, mfma, monkeypatch):
@@ -242,7 +242,8 @@ def test_fused_313_matches_generic_path(block, B, mfma, monkeypatch):
     and the log-det series of the full-size CIFAR nets.  Before every call the workspace and the
     LDS of every CU are filled with NaN, so a read of memory the kernels never wrote shows up as
     NaN deterministically (B=2 takes the 32-pixel split-K tiles, B=16 the 64-pixel tiles).  mfma selects the
-    fused kernel's arithmetic: 0 exact fp32 MFMA, 1 the split-bf16 ("x6") MFMA path."""
+    fused kernel's arithmetic: 0 exact fp32 MFMA, 1 the split-bf16 ("x6") MFMA path, 2 x6 with the scaled
+    two-piece fp16 phase B (INF_MFMA_F16X3)."""
     arch = syn.CIFAR10
     outs = {}
     for mode in ('fused', 'generic'):
@@ -291,7 +292,8 @@ def test_split_bf16_error_at_fp32_level(block):
     """INF_MFMA_BF16X6 (exact three-way bf16 split, six products per fp32 product) against INF_MFMA_F32 on the
     full-size CIFAR nets: both forward and VJP measured against an fp64 CPU evaluation of the same net.
     Tolerance: the split path's max error (relative to max|ref|) <= 1.5x the fp32 MFMA path's + 1e-7,
-    and both <= 2e-6 (fp32 roundoff level)."""
+    and both <= 2e-6 (fp32 roundoff level).  INF_MFMA_F16X3 (scaled two-piece fp16 phase B, three products):
+    <= 2x the fp32 MFMA path's + 2e-7, and <= 2e-6."""
     arch = syn.CIFAR10
     B = 4
     m, sd = _model(arch, B)
@@ -311,7 +313,7 @@ def test_split_bf16_error_at_fp32_level(block):
     net.refresh_if_needed(stream)
     ws = _hip.workspace(xd.device, net.ws_bytes(B))
     err = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         _hip.check(net.lib.inf_net_set_mfma(net.handle, mode), 'set_mfma')
         assert net.lib.inf_net_get_mfma(net.handle) == mode
         y = torch.empty_like(xd)
@@ -322,9 +324,11 @@ def test_split_bf16_error_at_fp32_level(block):
                                        ws.numel(), stream), 'vjp')
         torch.cuda.synchronize()
         err[mode] = [((a.double().cpu() - r).abs().max() / r.abs().max()).item() for a, r in ((y, y_ref), (g, g_ref))]
-    for e32, e6 in zip(err[0], err[1]):
-        assert e32 <= 2e-6 and e6 <= 2e-6, err
+    print('max error vs fp64 (fwd, vjp): f32 %s  bf16x6 %s  f16x3 %s' % (err[0], err[1], err[2]))
+    for e32, e6, e3 in zip(err[0], err[1], err[2]):
+        assert e32 <= 2e-6 and e6 <= 2e-6 and e3 <= 2e-6, err
         assert e6 <= 1.5 * e32 + 1e-7, err
+        assert e3 <= 2.0 * e32 + 2e-7, err
 
 
 @pytest.mark.parametrize('kind', ['conv3', 'conv1', 'linear', 'conv3_fixed', 'conv3_cifar'])
@@ -394,7 +398,7 @@ def test_update_lipschitz_batch_matches_per_layer():
 
 
 @pytest.mark.parametrize('C,H,hid,B', [(48, 64, 512, 2), (192, 32, 512, 2), (3, 32, 256, 8), (12, 16, 256, 2)])
-@pytest.mark.parametrize('mfma', [0, 1])
+@pytest.mark.parametrize('mfma', [0, 1, 2])
 def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
     """CelebA-HQ 256 scales (9C tap rows up to 1728, 64x64 / 32x32): the 32-pixel full-LDS variant
     (net313_kernel_w, several phase-C rounds) against the generic GEMM chain, workspace and LDS
