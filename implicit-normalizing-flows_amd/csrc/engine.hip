@@ -1923,4 +1923,9 @@ size_t inf_grad_workspace_bytes(InfNet* n, int B) {
 
 int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
 
+int inf_set_fused_k128(int policy) {
+  const int prev = inf::set_fused_k128(policy);
+  return prev < 0 ? -INF_ERR_INVALID : prev;
+}
+
 }  // extern "C"

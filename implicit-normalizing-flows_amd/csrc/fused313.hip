@@ -26,6 +26,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <map>
 #include <string>
 
@@ -1119,6 +1120,17 @@ static void timing_collect(const char* key, long nwg, hipStream_t s) {
   }
 }
 
+// VJP variant policy (inf_set_fused_k128): 0 the 64-pixel kernel only, 1 the 128-pixel K-chunked kernel where its
+// grid still covers every CU (default; INFLOW_FUSED_K128 in the environment), 2 wherever it fits (tests)
+static std::atomic<int> g_k128{[] {
+  const char* e = getenv("INFLOW_FUSED_K128");
+  return e ? atoi(e) : 1;
+}()};
+int set_fused_k128(int policy) {
+  if (policy < 0 || policy > 2) return -1;
+  return g_k128.exchange(policy);
+}
+
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets) {
   if (layout_nets <= 0) layout_nets = nnets;
   const Net313Args& a0 = args[0];
@@ -1147,8 +1159,16 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   Net313Pair pr;
   pr.a[0] = args[0];
   pr.a[1] = args[nnets - 1];
-  for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < bn ? a0.W : bn;
-  pr.nb0 = a0.B * (P / bn);
+  const bool h3_args = pr.a[0].A1h != nullptr && pr.a[1].A1h != nullptr && pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr;
+  // 128-pixel K-chunked VJP (fused313k.hip): h3 (all phases), where the pair's derivatives are in the 64-pixel
+  // layout and the grid still covers every CU
+  const int k128_pol = g_k128.load(std::memory_order_relaxed);
+  const bool k128 = k128_pol && H3_AC && h3_args && mode == MODE_VJP && var == V64 && force_bn == 0 &&
+                    force_var < 0 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
+                    (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
+  const int tbn = k128 ? 128 : bn;
+  for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < tbn ? a0.W : tbn;
+  pr.nb0 = a0.B * (P / tbn);
   static const int max_ksplit = [] {
     const char* ks = getenv("INFLOW_FUSED_KSPLIT");     // debug knob: cap phase C's K split
     const int v = ks ? atoi(ks) : 8;
@@ -1177,6 +1197,21 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool quad = quad_env == 4;
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
+  if (k128) {
+    INF_TRY(launch_net313k_vjp(pr, nb, s));
+    if (pr.tbuf) {
+      char key[64];
+      snprintf(key, sizeof(key), "var3 mode%d split2 C%d", mode, a0.C);
+      timing_collect(key, (long)nb, s);
+    }
+    if (prof) {
+      const double npx = (double)nnets * a0.B * P;
+      const double f = 2.0 * hid * 9.0 * a0.C * 2.0 + 2.0 * hid * hid;
+      const double bytes = 4.0 * npx * (a0.C + 2.0 * hid + 9.0 * a0.C);
+      prof_end_launch(s, 532, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+    }
+    return INF_OK;
+  }
 #define L313S(TM_, MODE_, SPL_)                                                                         \
   do {                                                                                                  \
     if (var == V64 && quad && SPL_ < 2) hipLaunchKernelGGL((net313_kernel_q<TM_, MODE_, (SPL_ < 2 ? SPL_ : 1)>), dim3(nb), dim3(256), 0, s, pr); \

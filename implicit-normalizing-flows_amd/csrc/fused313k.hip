@@ -1,0 +1,540 @@
+// 128-pixel, K-chunked variant of the fused 3-1-3 VJP (fused313.hip), INF_MFMA_F16X3 only.
+//
+// Why: with the scaled fp16 split, phase B of the 64-pixel kernel is bound by its weight-operand stream
+// (1 MiB of h/l planes per 64-pixel tile, ~21 B/clk/CU measured under both split modes), not by the MFMA
+// pipe.  Twice the pixels per workgroup halves the weight bytes per pixel, but a 512 x 128 fp32
+// activation tile (256 KiB) does not fit the 160 KiB LDS.  So the HID dimension is cut into two 256-row
+// chunks, and each chunk of an activation goes through LDS once, already split into the fp16 (h, l)
+// planes phase B / C consume (128 KiB per chunk):
+//
+//   stage halo (series chaining as in fused313.hip)
+//   for chunk c in {0, 1}:
+//     phase A rows [256c, 256c + 256): t = (W_A^T-flipped . im2col(v)) * d2        (per wave 32 rows)
+//     per-column scale over the chunk, split -> LDS chunk buffer                    (2 barriers)
+//     phase B, K = the chunk's 256 rows: acc += W_B^T[:, chunk] . t_chunk            (per wave 64 x 128)
+//   t2 = acc * d1; per-column scale over all 512 rows
+//   for chunk c in {0, 1}: waves holding rows of c split them -> LDS; phase C over the chunk's K tiles
+//   (split-K partials reduced through LDS) -> packed taps Y
+//
+// The phase-B B operand is two ds_read_b128 per 32-pixel column and K tile (no split VALU in the loop),
+// and each weight fragment feeds 4 column blocks (24 MFMAs per 4 KiB of weight loads per wave).
+// Chunk scales: each chunk has its own power-of-two column scale; the phase-B accumulator is moved to the
+// second chunk's scale by an exact ldexp between the chunks (the two exponents are kept within 60 of
+// each other, so no finite partial sum over- or underflows).
+// d1 / d2 are read in the 64-pixel kernel's fragment layout (the SAVE launches of the pair write them):
+// 128-pixel tile t covers 64-pixel tiles 2t, 2t + 1.
+#include <type_traits>
+
+#include "kernels.h"
+
+namespace inf {
+
+namespace {
+constexpr int KB_BN = 128;          // pixels per tile
+constexpr int KB_NB = 4;            // 32-pixel column blocks
+constexpr int KB_NW = 8;            // waves
+constexpr int KB_NT = 64 * KB_NW;
+constexpr int KB_HID = 512;
+constexpr int KB_LDS = 40960;       // floats (160 KiB)
+constexpr int KB_CHUNK = 32768;     // floats: 16 K tiles x 4 column blocks x 2 planes x 64 lanes x 16 B
+constexpr int KB_TSLOTS = 32;
+
+// the two (h, l) planes of fragment tile `tile` (fragment-major, launch_split2h order)
+__device__ __forceinline__ void ldw2(const u32x4* base, long tile, int lane, u32x4 (&o)[2]) {
+  const u32x4* q = base + tile * 2 * 64 + lane;
+  o[0] = q[0];
+  o[1] = q[64];
+}
+
+// 4 consecutive fp32 values (rows q = 0..3 of one accumulator group) -> scaled fp16 h / l pieces, packed
+__device__ __forceinline__ void split4h(float v0, float v1, float v2, float v3, float S, uint2& h, uint2& l) {
+  const _Float16 h0 = (_Float16)(v0 * S), h1 = (_Float16)(v1 * S), h2 = (_Float16)(v2 * S), h3 = (_Float16)(v3 * S);
+  const _Float16 l0 = (_Float16)__builtin_fmaf(v0, S, -(float)h0), l1 = (_Float16)__builtin_fmaf(v1, S, -(float)h1);
+  const _Float16 l2 = (_Float16)__builtin_fmaf(v2, S, -(float)h2), l3 = (_Float16)__builtin_fmaf(v3, S, -(float)h3);
+  const f16x2 a = {h0, h1}, b = {h2, h3}, c = {l0, l1}, d = {l2, l3};
+  h = make_uint2(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b));
+  l = make_uint2(__builtin_bit_cast(unsigned, c), __builtin_bit_cast(unsigned, d));
+}
+}  // namespace
+
+// 128-pixel tiles fit: whole image rows (or a 128-wide row segment), halo + im2col table + chunk buffer
+int net313k_fits(int hid, int C, int H, int W) {
+  if (hid != KB_HID) return 0;
+  const int P = H * W;
+  const int seg = W < KB_BN ? W : KB_BN;
+  if (P % KB_BN != 0 || KB_BN % seg != 0 || (W > KB_BN && W % KB_BN != 0)) return 0;
+  if (9 * C > 256) return 0;                      // phase C: at most 8 row blocks x 4 columns = 4 jobs per wave
+  const int rows = KB_BN / seg;
+  const long k1pad = (9L * C + 15) / 16 * 16;
+  const long need = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
+  return need <= KB_LDS;
+}
+
+__global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
+  const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
+  const Net313Args& a = pr.a[sel];
+  const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
+  __shared__ __attribute__((aligned(16))) float smem[KB_LDS];
+#define KSTAMP(i_)                                                                             \
+  do {                                                                                         \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  KSTAMP(0);
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int P = a.H * a.W;
+  const int tiles_per_img = P / KB_BN;
+  const int img = bid / tiles_per_img, tile = bid - img * tiles_per_img;
+  const int p0 = tile * KB_BN;
+  const int seg = a.seg, rows = KB_BN / seg;
+  const int y0 = p0 / a.W, x0 = p0 - y0 * a.W;
+  const int RH = rows + 2, CW = seg + 2;
+  const int vhn = a.C * RH * CW;
+  const int vhz = vhn + rows * CW;                  // zero run for the K-padding rows of phase A
+  // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] | trace partials [NW] (fp64) | koff | halo
+  u32x4* cb = reinterpret_cast<u32x4*>(smem);
+  float* cmax = smem + KB_CHUNK;
+  float* hmax = cmax + KB_NW * KB_BN;
+  double* red = reinterpret_cast<double*>(hmax + 8);
+  int* koff = reinterpret_cast<int*>(red + KB_NW);
+  float* vh = reinterpret_cast<float*>(koff + a.K1pad);
+
+  // d1 / d2 in the 64-pixel kernel's fragment order: 64-px tile (2 tile + b / 2), column (b & 1), row block rb
+  const long tile64 = (long)img * (P / 64) + 2 * tile;
+  auto dptr = [&](const float* base, int rb, int b) {
+    return reinterpret_cast<const f32x4*>(base + (((tile64 + (b >> 1)) * 16 + rb) * 2 + (b & 1)) * 1024 + lane * 16);
+  };
+  // phase A's multiplier d2 for one chunk (this wave's 32 rows x 128 pixels), requested ahead of its use: chunk 0's
+  // before the staging; chunk 1's first two column blocks right after phase B of chunk 0 (the registers beside
+  // the phase-B accumulators allow 32), its last two at the start of phase A
+  f32x4 d2v[KB_NB][4];
+  auto loadD2 = [&](int c, int b0, int b1) {
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b) {
+      if (b < b0 || b >= b1) continue;
+      const f32x4* q = dptr(a.d2, 8 * c + wid, b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d2v[b][j] = q[j];
+    }
+  };
+  loadD2(0, 0, KB_NB);
+
+  // ---- stage the input halo tile (series chaining: tap sum, preact swish', trace partial / Neumann acc) ----
+  float hmx = 0.f;
+  double dacc = 0.0;
+  {
+    const float* in = a.in ? a.in + (long)img * a.C * P : nullptr;
+    if (a.in_taps) {
+      const float* ytap = a.in_taps + (long)img * a.M3 * P;
+      const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
+      const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
+      const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
+      const float* mxp = mx ? mx : ytap;
+      const float* epp = ep ? ep : ytap;
+      float* accw = a.acc_w ? a.acc_w + (long)img * a.C * P : nullptr;
+      const float* awp = accw ? accw : ytap;
+      auto pass = [&](auto nuc, int i0) {
+        constexpr int NU = decltype(nuc)::value;
+        float tv[NU][9], xm[NU], ev[NU], wv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int i = i0 + u * KB_NT;
+          const int ic = i < vhn ? i : 0;
+          const int c = ic / (RH * CW), rr = ic - c * RH * CW;
+          const int hy = rr / CW, hx = rr - hy * CW;
+          const int yq = min(max(y0 + hy - 1, 0), a.H - 1), xq = min(max(x0 + hx - 1, 0), a.W - 1);
+          const long ee = (long)c * P + yq * a.W + xq;
+          const float* yc = ytap + (long)c * 9 * P;
+#pragma unroll
+          for (int tp = 0; tp < 9; ++tp) {
+            const int y2 = min(max(yq + tp / 3 - 1, 0), a.H - 1), x2 = min(max(xq + tp % 3 - 1, 0), a.W - 1);
+            tv[u][tp] = yc[(long)tp * P + y2 * a.W + x2];
+          }
+          xm[u] = mxp[ee];
+          ev[u] = epp[ee];
+          wv[u] = awp[ee];
+        }
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int i = i0 + u * KB_NT;
+          const int ic = i < vhn ? i : 0;
+          const int rr = ic % (RH * CW);
+          const int hy = rr / CW, hx = rr - hy * CW;
+          const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+          const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+          const int ok = in_img ? ((hy >= 1 && hy <= rows && hx >= 1 && hx <= seg) ? 2 : 1) : 0;
+          float v = 0.f;
+#pragma unroll
+          for (int tp = 0; tp < 9; ++tp) {
+            const int y2 = yy + tp / 3 - 1, x2 = xx + tp % 3 - 1;
+            const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
+            v += vt ? tv[u][tp] : 0.f;
+          }
+          if (mx) v = v * swish_d(xm[u], msp);
+          v = ok ? v : 0.f;
+          if (ep && ok == 2) dacc += (double)v * (double)ev[u];
+          if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
+          hmx = fmaxf(hmx, fabsf(v));
+          if (i < vhz) vh[i] = v;
+        }
+      };
+      constexpr int SU = 2;     // (2 halo elements per pass: d2 of chunk 0 is already in flight beside them)
+      for (int i0 = tid; i0 < vhz; i0 += KB_NT * SU) {
+        const int nu = min(SU, (vhz - (i0 - tid) + KB_NT - 1) / KB_NT);     // wave-uniform
+        if (nu >= 2) pass(std::integral_constant<int, 2>(), i0);
+        else pass(std::integral_constant<int, 1>(), i0);
+      }
+    } else {
+      const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+      for (int i = tid; i < vhz; i += KB_NT) {
+        float v = 0.f;
+        if (i < vhn) {
+          const int c = i / (RH * CW), rr = i - c * RH * CW;
+          const int hy = rr / CW, hx = rr - hy * CW;
+          const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+          if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+            v = in[(long)c * P + yy * a.W + xx];
+            if (a.pre_beta) v = swish_f(v, pre_sp);
+          }
+        }
+        hmx = fmaxf(hmx, fabsf(v));
+        vh[i] = v;
+      }
+    }
+  }
+  {
+    const float w = wave_max(hmx);
+    if (lane == 0) hmax[wid] = w;
+  }
+  if (a.dot_part) {
+    const double w = wave_sum(dacc);
+    if (lane == 0) red[wid] = w;
+  }
+  for (int k = tid; k < a.K1pad; k += KB_NT) {
+    int o = vhn;                                    // zero run for the K padding
+    if (k < 9 * a.C) {
+      const int c = k / 9, tt = k - c * 9;
+      o = c * RH * CW + (tt / 3) * CW + (tt % 3);
+    }
+    koff[k] = o;
+  }
+  int pix[KB_NB];
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) {
+    const int n = b * 32 + li;
+    const int py = n / seg;
+    pix[b] = py * CW + (n - py * seg);
+  }
+  __syncthreads();
+  KSTAMP(1);
+  if (a.dot_part && tid == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < KB_NW; ++w) s += red[w];
+    a.dot_part[(long)img * a.dot_nchunk + tile] = s;
+  }
+  // phase A scale: one per tile (halo max over all waves)
+  float sA;
+  int eA;
+  {
+    float m_ = 0.f;
+#pragma unroll
+    for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, hmax[w]);
+    const int sc = h3_scale_exp(m_);
+    sA = __builtin_amdgcn_ldexpf(1.f, sc);
+    eA = -(sc + a.Ah_exp[0]);
+  }
+  const u32x4* A1h = reinterpret_cast<const u32x4*>(a.A1h);
+  const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);
+  const u32x4* A3h = reinterpret_cast<const u32x4*>(a.A3h);
+  const int nkt1 = a.K1pad / 16;
+  const int ew = a.Ah_exp[1];
+
+  // writes this wave's values of one 32-row block (rows kt0 * 16 .. + 31 of the chunk) and column block b
+  // into the chunk buffer: accumulator group g holds rows 8g + 4 lh + q, which consumer lane 32 (g & 1) + li
+  // reads as its k-slots 4 lh + q of K tile kt0 + (g >> 1)
+  auto put = [&](int kt0, int b, const float (&v)[16], float S) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint2 h, l;
+      split4h(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3], S, h, l);
+      const int kt = kt0 + (g >> 1);
+      const int base = ((kt * KB_NB + b) * 2) * 64 + 32 * (g & 1) + li;
+      reinterpret_cast<uint2*>(cb + base)[lh] = h;
+      reinterpret_cast<uint2*>(cb + base + 64)[lh] = l;
+    }
+  };
+
+  f32x16 acc[2][KB_NB];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][b][r] = 0.f;
+  int scB[KB_NB];                                    // phase-B column scale exponent of the current chunk
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) scB[b] = 0;
+
+  // the two chunks as separate code (chunk 0 starts from known-zero accumulators)
+  auto chunk = [&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    if constexpr (c == 1) loadD2(1, 2, KB_NB);
+    // ------------------------------------------------ phase A, rows of this wave in chunk c (row block 8c + wid)
+    const int rbA = 8 * c + wid;
+    float va[KB_NB][16];
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b) {
+      f32x16 ac;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ac[r] = 0.f;
+      u32x4 w0[2], w1[2];
+      ldw2(A1h, (long)rbA * nkt1, lane, w0);
+      auto stepA = [&](int kt, const u32x4 (&af)[2]) {
+        const int* kp = koff + kt * 16 + lh * 8;
+        const int4 k0 = *reinterpret_cast<const int4*>(kp);
+        const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
+        const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+        float x[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x[kk] = vh[ko[kk] + pix[b]];
+        u32x4 h, l;
+        split2h(x, sA, h, l);
+        ac = mfma_h3(af, h, l, ac);
+      };
+      for (int kt = 0; kt < nkt1; kt += 2) {
+        const bool has1 = kt + 1 < nkt1;
+        if (has1) ldw2(A1h, (long)rbA * nkt1 + kt + 1, lane, w1);
+        stepA(kt, w0);
+        if (kt + 2 < nkt1) ldw2(A1h, (long)rbA * nkt1 + kt + 2, lane, w0);
+        if (has1) stepA(kt + 1, w1);
+      }
+      // epilogue A: unscale, times d2 = swish'(a2) (the VJP through the second activation)
+      float cm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 d = d2v[b][j];
+        va[b][4 * j] = __builtin_amdgcn_ldexpf(ac[4 * j], eA) * d.x;
+        va[b][4 * j + 1] = __builtin_amdgcn_ldexpf(ac[4 * j + 1], eA) * d.y;
+        va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[4 * j + 2], eA) * d.z;
+        va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[4 * j + 3], eA) * d.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;
+    }
+    __syncthreads();      // column maxima visible; every wave is done reading the previous chunk buffer
+    if (c == 0) KSTAMP(2);
+    // chunk column scales; chunk 1 stays within 2^60 of chunk 0 and the accumulator moves to its scale
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b) {
+      float m_ = 0.f;
+#pragma unroll
+      for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, cmax[w * KB_BN + b * 32 + li]);
+      int sc = h3_scale_exp(m_);
+      if constexpr (c == 1) {
+        sc = min(max(sc, scB[b] - 60), scB[b] + 60);
+        const int de = sc - scB[b];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], de);
+      }
+      scB[b] = sc;
+      put(2 * wid, b, va[b], __builtin_amdgcn_ldexpf(1.f, sc));
+    }
+    __syncthreads();      // chunk buffer complete
+    if (c == 0) KSTAMP(3);
+    // ------------------------------------------------ phase B over the chunk's 16 K tiles
+    {
+      const int rbw = 2 * wid;
+      auto ldB = [&](int kt, u32x4 (&h)[KB_NB], u32x4 (&l)[KB_NB]) {
+#pragma unroll
+        for (int b = 0; b < KB_NB; ++b) {
+          h[b] = cb[((kt * KB_NB + b) * 2) * 64 + lane];
+          l[b] = cb[((kt * KB_NB + b) * 2 + 1) * 64 + lane];
+        }
+      };
+      auto ldW = [&](int kt, u32x4 (&o)[2][2]) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) ldw2(A2h, (long)(rbw + m) * 32 + 16 * c + kt, lane, o[m]);
+      };
+      // one B fragment pair per column block, re-read for the next K tile right after its MFMAs issue
+      auto mmr = [&](const u32x4 (&w)[2][2], u32x4 (&h)[KB_NB], u32x4 (&l)[KB_NB], int kn) {
+#pragma unroll
+        for (int b = 0; b < KB_NB; ++b) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m) acc[m][b] = mfma_h3(w[m], h[b], l[b], acc[m][b]);
+          h[b] = cb[((kn * KB_NB + b) * 2) * 64 + lane];
+          l[b] = cb[((kn * KB_NB + b) * 2 + 1) * 64 + lane];
+        }
+      };
+      u32x4 wa[2][2], wb[2][2], hb[KB_NB], lb[KB_NB];
+      ldW(0, wa);
+      ldB(0, hb, lb);
+      for (int kt = 0; kt < 16; kt += 2) {
+        ldW(kt + 1, wb);
+        mmr(wa, hb, lb, kt + 1);
+        if (kt + 2 < 16) ldW(kt + 2, wa);
+        mmr(wb, hb, lb, min(kt + 2, 15));
+      }
+    }
+    if constexpr (c == 0) {
+      KSTAMP(4);
+      loadD2(1, 0, 2);
+    }
+  };
+  chunk(std::integral_constant<int, 0>());
+  chunk(std::integral_constant<int, 1>());
+  KSTAMP(5);
+  // ------------------------------------------------ epilogue B: unscale, times d1 = swish'(a1)
+  float cmC[KB_NB];
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) cmC[b] = 0.f;
+  // (one row block at a time: its 4 column blocks' d1 requested together, 64 registers)
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    f32x4 d1v[KB_NB][4];
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b) {
+      const f32x4* q = dptr(a.d1, 2 * wid + m, b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];
+    }
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b) {
+      const int e = -(scB[b] + ew);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 d = d1v[b][j];
+        acc[m][b][4 * j] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j], e) * d.x;
+        acc[m][b][4 * j + 1] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j + 1], e) * d.y;
+        acc[m][b][4 * j + 2] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j + 2], e) * d.z;
+        acc[m][b][4 * j + 3] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j + 3], e) * d.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) {
+    const float cm = fmaxf(cmC[b], __shfl_xor(cmC[b], 32, 64));
+    if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;   // (free: every wave read it before the last barrier)
+  }
+  __syncthreads();        // column maxima of t2 visible; every wave is done with the phase-B chunk buffer
+  float sC[KB_NB];
+  int eC[KB_NB];
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) {
+    float m_ = 0.f;
+#pragma unroll
+    for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, cmax[w * KB_BN + b * 32 + li]);
+    const int sc = h3_scale_exp(m_);
+    sC[b] = __builtin_amdgcn_ldexpf(1.f, sc);
+    eC[b] = -(sc + a.Ah_exp[2]);
+  }
+  // ------------------------------------------------ phase C: jobs = (row block of the 9C taps) x column block
+  const int nrb = a.M3pad / 32;
+  const int ntask = nrb * KB_NB;
+  int ksplit = 1;
+  while (ntask * ksplit * 2 <= KB_NW) ksplit *= 2;
+  const int kts = 16 / ksplit;                       // K tiles per job and chunk
+  const int njobs = ntask * ksplit;                  // <= 32 (net313k_fits)
+  f32x16 cacc[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
+  // with ksplit == 1 a wave's jobs (wid + 8 jj) share the column block wid % 4; with ksplit > 1 one job each
+  const int job0 = wid;
+  const int ks = job0 % ksplit;
+  const int bC = (job0 / ksplit) % KB_NB;
+#pragma unroll 1
+  for (int c = 0; c < 2; ++c) {
+    if (wid / 4 == c) {                                // this wave's t2 rows belong to chunk c
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int b = 0; b < KB_NB; ++b) {
+          float v[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = acc[m][b][r];
+          put(4 * (wid & 3) + 2 * m, b, v, sC[b]);
+        }
+    }
+    __syncthreads();
+    if (c == 0) KSTAMP(6);
+    const int k_lo = ks * kts;
+    for (int jj = 0; jj < 4; ++jj) {
+      const int job = job0 + KB_NW * jj;
+      if (job >= njobs) break;
+      const int rb = (job / ksplit) / KB_NB;
+      u32x4 w0[2], w1[2];
+      ldw2(A3h, (long)rb * 32 + 16 * c + k_lo, lane, w0);
+      for (int kt = k_lo; kt < k_lo + kts; kt += 2) {
+        ldw2(A3h, (long)rb * 32 + 16 * c + kt + 1, lane, w1);
+        {
+          const u32x4 h = cb[((kt * KB_NB + bC) * 2) * 64 + lane], l = cb[((kt * KB_NB + bC) * 2 + 1) * 64 + lane];
+          cacc[jj] = mfma_h3(w0, h, l, cacc[jj]);
+        }
+        if (kt + 2 < k_lo + kts) ldw2(A3h, (long)rb * 32 + 16 * c + kt + 2, lane, w0);
+        {
+          const u32x4 h = cb[(((kt + 1) * KB_NB + bC) * 2) * 64 + lane], l = cb[(((kt + 1) * KB_NB + bC) * 2 + 1) * 64 + lane];
+          cacc[jj] = mfma_h3(w1, h, l, cacc[jj]);
+        }
+      }
+    }
+    if (c == 0) __syncthreads();                       // chunk 1's rows overwrite the buffer
+  }
+  KSTAMP(7);
+  float* Y = a.Y + (long)img * a.M3 * P;
+  const int n_out = bC * 32 + li, py_out = n_out / seg;
+  const int gcol = (y0 + py_out) * a.W + x0 + (n_out - py_out * seg);
+  int eCj = 0;                                       // unscale exponent of this wave's column block
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) eCj = b == bC ? eC[b] : eCj;
+  if (ksplit == 1) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int job = job0 + KB_NW * jj;
+      if (job >= njobs) break;
+      const int rb = job / KB_NB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.M3) Y[(long)row * P + gcol] = __builtin_amdgcn_ldexpf(cacc[jj][r], eCj);
+      }
+    }
+  } else {
+    float* part = smem;                                // the chunk buffer is free after this barrier
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[(job0 * 16 + r) * 64 + lane] = __builtin_amdgcn_ldexpf(cacc[0][r], eCj);
+    __syncthreads();
+    for (int i = tid; i < ntask * 1024; i += KB_NT) {
+      const int task = i >> 10, rem = i & 1023, r = rem >> 6, ln = rem & 63;
+      float sum = 0.f;
+      for (int k = 0; k < ksplit; ++k) sum += part[((task * ksplit + k) * 16 + r) * 64 + ln];
+      const int rb = task / KB_NB, b = task % KB_NB;
+      const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+      const int n = b * 32 + (ln & 31), py = n / seg;
+      if (row < a.M3) Y[(long)row * P + (y0 + py) * a.W + x0 + (n - py * seg)] = sum;
+    }
+  }
+  if (pr.tbuf && threadIdx.x == 0) {
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+    pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
+    for (int v = 0; v < 16; ++v) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + v] = t_;
+  }
+#undef KSTAMP
+}
+
+int launch_net313k_vjp(const Net313Pair& pr, unsigned nb, hipStream_t s) {
+  hipLaunchKernelGGL(net313k_vjp_kernel, dim3(nb), dim3(KB_NT), 0, s, pr);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+}  // namespace inf

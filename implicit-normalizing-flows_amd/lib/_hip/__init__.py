@@ -112,6 +112,7 @@ _SIGS = {
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
+    'inf_set_fused_k128': (ctypes.c_int, [ctypes.c_int]),
     'inf_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int]),
     'inf_net_param_grad': (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t,
                                           _P]),
@@ -327,8 +328,10 @@ def profile_end():
 
 def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
-    if 500 <= tag < 530:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide)
-        return 'net313_kernel%s<%s>' % (['', '_h', '_w'][(tag - 500) // 10], ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
+    if 500 <= tag < 540:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide),
+        #                      53x: net313k (128-px K-chunked VJP, fused313k.hip)
+        return 'net313%s<%s>' % (['_kernel', '_kernel_h', '_kernel_w', 'k_kernel'][(tag - 500) // 10],
+                                 ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
     if tag == 899:
         return 'wgrad_valu_kernel'
     if 800 <= tag < 900:     # weight-gradient kernel (grad.hip), 8<TMW><TNW>

@@ -448,3 +448,59 @@ def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
         assert torch.isfinite(a).all()
     for a, b in zip(outs['fused'], outs['generic']):
         _close(a, b, rel=1e-5)
+
+
+@pytest.mark.parametrize('B', [2, 16])
+@pytest.mark.parametrize('block', [0, 1, 3])
+def test_fused_k128_vjp_matches_64px_kernel(block, B):
+    """The 128-pixel K-chunked VJP (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
+    256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net VJP, the chained log-det
+    series (each term stages the previous term's taps, preact swish' and trace partial) and the Neumann vector
+    (each term stages the accumulation w += c_k v_k), with the workspace and every CU's LDS NaN-poisoned before
+    each call.  inf_set_fused_k128(2) forces the 128-pixel kernel at these small grids.  Tolerance: 1e-5 of
+    max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons."""
+    arch = syn.CIFAR10
+    m, _ = _model(arch, B)
+    blk = imblocks(m)[block]
+    shape = blk.nnet_x[-1].weight.shape[0], 32 >> (block // 2), 32 >> (block // 2)
+    torch.manual_seed(7)
+    x = (torch.randn(B, *shape) * 0.5).to(DEV)
+    v = torch.randn(B, *shape).to(DEV)
+    eps = torch.sign(v)
+    net = _hip.native_net(blk.nnet_z, x.shape[1:], x.device)
+    _hip.check(net.lib.inf_net_set_mfma(net.handle, 2), 'set_mfma')
+    stream = _hip.stream_of(x)
+    net.refresh_if_needed(stream)
+    ws = _hip.workspace(x.device, net.ws_bytes(B))
+    n = 10
+    co = np.array([(-1) ** (k + 1) / k for k in range(1, n + 1)], dtype=np.float32)
+    nco = np.array([(-1) ** k * (1.0 if k < 8 else 0.5) for k in range(n + 1)], dtype=np.float32)
+    fptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+    def poison():
+        ws.fill_(255)
+        _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
+    outs = {}
+    try:
+        for pol in (2, 0):
+            prev = net.lib.inf_set_fused_k128(pol)
+            assert prev in (0, 1, 2)
+            g, ld, w = torch.empty_like(x), torch.empty(B, device=DEV), torch.empty_like(x)
+            poison()
+            _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(x), _hip.ptr(v), _hip.ptr(g), B, _hip.ptr(ws),
+                                           ws.numel(), stream), 'vjp')
+            poison()
+            _hip.check(net.lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(eps), fptr(co), n, _hip.ptr(ld), B,
+                                                 _hip.ptr(ws), ws.numel(), stream), 'series')
+            poison()
+            _hip.check(net.lib.inf_neumann_vector(net.handle, _hip.ptr(x), _hip.ptr(eps), fptr(nco), n, _hip.ptr(w), B,
+                                                  _hip.ptr(ws), ws.numel(), stream), 'neumann')
+            torch.cuda.synchronize()
+            outs[pol] = (g, ld, w)
+    finally:
+        net.lib.inf_set_fused_k128(1)
+    assert net.lib.inf_set_fused_k128(3) < 0
+    for a in outs[2]:
+        assert torch.isfinite(a).all()
+    for a, b in zip(outs[2], outs[0]):
+        _close(a, b, rel=1e-5)
