@@ -43,9 +43,6 @@ METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs 
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA peak (1024 flop/clk/SIMD x 1024 SIMDs x 2.4 GHz)
-# The fused net kernel's default arithmetic (INF_MFMA_BF16X6, include/inflow.h): every fp32 operand split exactly
-# into three bf16 pieces, six bf16 MFMA products per fp32 product -> fp32-equivalent peak = bf16 peak / 6.
-X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 
 
 def mfma_mode():
@@ -170,13 +167,19 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- live per-kernel timing (one extra step, outside the timed region) ----
+    # The timed steps run the overlapped eval schedule (inf_set_eval_overlap: x-branch series on a side stream);
+    # this step runs the sequential one, so each kernel's HIP-event duration is its own, not shared with a
+    # concurrent launch (tools/profile_round.sh runs rocprofv3 with INFLOW_EVAL_OVERLAP=0 to match).
     steps_info = [b.last_broyden['nstep'] for b in imblocks(model)]
+    lib = _hip.load()
+    overlap_prev = lib.inf_set_eval_overlap(0)
     _hip.profile_begin(100000)
     t1 = time.perf_counter()
     step(0)
     torch.cuda.synchronize()
     prof_wall = time.perf_counter() - t1
     stats = _hip.profile_end()
+    lib.inf_set_eval_overlap(overlap_prev)
     nps = [getattr(b, 'last_n_power_series', None) for b in imblocks(model)]
     gemms = [s for s in stats if s['flops'] > 0]          # MFMA kernels (GEMM family + fused net)
     dom = max(gemms, key=lambda s: s['total_ms'])
@@ -224,6 +227,9 @@ def main():
                                     '3 in f16x3 phases; f32 %.1f TF)' % (BF16_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS)),
                      'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not MFMA instruction FLOPs',
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
+                     'schedule': 'per-kernel durations from one extra step on the sequential eval schedule (timed '
+                                 'steps: %s)' % ('x-branch series on a side stream' if overlap_prev == 1
+                                                else 'sequential'),
                      'flops_per_launch': dom['flops'] / dom['launches']},
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),
                  'gemm_flop_rate_tflops': round(total_gemm_flops / (prof_wall * 1e12), 2),

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <functional>
 #include <vector>
@@ -1400,6 +1401,12 @@ static SideStream* side_stream() {
   return &ss;
 }
 
+// inf_set_eval_overlap: process-wide switch of the overlapped eval schedule below
+static std::atomic<int> g_eval_overlap{[] {
+  const char* e = getenv("INFLOW_EVAL_OVERLAP");
+  return e ? (e[0] == '1' ? 1 : 0) : 1;
+}()};
+
 // Whole eval pass of an imBlock on fused nets (implicit_block.py:220-234 + 245-322 in eval): the x-net's
 // x_embed launch also saves its activation derivatives at x (MODE_EVALSAVE), Broyden solves for z*,
 // z = (f_x(x) - f_z(z*)) + x, then the paired power series of both branches with only the z-net's SAVE.
@@ -1417,16 +1424,12 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
   Bufs bfa, bfb, bfc;
   carve(nx, B, T, w0, half, bfa);
   carve(nz, B, 1, w0 + half, zneed, bfb);
-  // Overlapped schedule (INFLOW_EVAL_OVERLAP=1 and workspace for a third region): the x-branch series
-  // depends only on x, so it runs on a side stream while this stream does the root solve (sync-bound, and
-  // short of work at the 8x8 scale) and then the z-branch series; the two streams join before returning.
-  // Measured +3 % samples/s at B=64, none at B=256; off by default because concurrent launches make
-  // per-kernel durations (bench roofline, rocprof averages) describe two kernels sharing the GPU.
-  static const bool overlap_env = [] {
-    const char* e = getenv("INFLOW_EVAL_OVERLAP");
-    return e && e[0] == '1';
-  }();
-  const bool overlap = overlap_env && ws_bytes >= half + zneed + xneed;
+  // Overlapped schedule (default; inf_set_eval_overlap / INFLOW_EVAL_OVERLAP=0 turn it off; needs workspace for a
+  // third region): the x-branch series depends only on x, so it runs on a side stream while this stream does the
+  // root solve (sync-bound, and short of work at the 8x8 scale) and then the z-branch series; the two streams join
+  // before returning.  Concurrent series launches also desynchronise the CUs' d1/d2 bursts (every 1-WG/CU tile
+  // of one launch reads its derivatives in the same phase): 2268 -> 2432 samples/s at B=64 with the 128-pixel VJP.
+  const bool overlap = g_eval_overlap.load(std::memory_order_relaxed) && ws_bytes >= half + zneed + xneed;
   if (overlap) {
     carve(nx, B, 1, w0 + half + zneed, xneed, bfc);
     bfc.D = bfa.D;                              // the x_embed pass saves f_x's derivatives into bfa.D
@@ -1922,6 +1925,11 @@ size_t inf_grad_workspace_bytes(InfNet* n, int B) {
 }
 
 int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
+
+int inf_set_eval_overlap(int on) {
+  if (on != 0 && on != 1) return -INF_ERR_INVALID;
+  return g_eval_overlap.exchange(on);
+}
 
 int inf_set_fused_k128(int policy) {
   const int prev = inf::set_fused_k128(policy);

@@ -179,10 +179,12 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
           if (i < vhz) vh[i] = v;
         }
       };
-      constexpr int SU = 2;     // (2 halo elements per pass: d2 of chunk 0 is already in flight beside them)
+      constexpr int SU = 4;
       for (int i0 = tid; i0 < vhz; i0 += KB_NT * SU) {
         const int nu = min(SU, (vhz - (i0 - tid) + KB_NT - 1) / KB_NT);     // wave-uniform
-        if (nu >= 2) pass(std::integral_constant<int, 2>(), i0);
+        if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
+        else if (nu == 3) pass(std::integral_constant<int, 3>(), i0);
+        else if (nu == 2) pass(std::integral_constant<int, 2>(), i0);
         else pass(std::integral_constant<int, 1>(), i0);
       }
     } else {
@@ -284,11 +286,14 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
     // ------------------------------------------------ phase A, rows of this wave in chunk c (row block 8c + wid)
     const int rbA = 8 * c + wid;
     float va[KB_NB][16];
+    // G column blocks b0 .. b0 + G - 1 over the K tiles in one sweep (each weight fragment used G times)
+    auto phaseA = [&](auto gc, auto bc) {
+      constexpr int G = decltype(gc)::value, b0 = decltype(bc)::value;
+      f32x16 ac[G];
 #pragma unroll
-    for (int b = 0; b < KB_NB; ++b) {
-      f32x16 ac;
+      for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ac[r] = 0.f;
+        for (int r = 0; r < 16; ++r) ac[g][r] = 0.f;
       u32x4 w0[2], w1[2];
       ldw2(A1h, (long)rbA * nkt1, lane, w0);
       auto stepA = [&](int kt, const u32x4 (&af)[2]) {
@@ -296,12 +301,15 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
         const int4 k0 = *reinterpret_cast<const int4*>(kp);
         const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
         const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-        float x[8];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) x[kk] = vh[ko[kk] + pix[b]];
-        u32x4 h, l;
-        split2h(x, sA, h, l);
-        ac = mfma_h3(af, h, l, ac);
+        for (int g = 0; g < G; ++g) {
+          float x[8];
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) x[kk] = vh[ko[kk] + pix[b0 + g]];
+          u32x4 h, l;
+          split2h(x, sA, h, l);
+          ac[g] = mfma_h3(af, h, l, ac[g]);
+        }
       };
       for (int kt = 0; kt < nkt1; kt += 2) {
         const bool has1 = kt + 1 < nkt1;
@@ -311,19 +319,33 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
         if (has1) stepA(kt + 1, w1);
       }
       // epilogue A: unscale, times d2 = swish'(a2) (the VJP through the second activation)
-      float cm = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 d = d2v[b][j];
-        va[b][4 * j] = __builtin_amdgcn_ldexpf(ac[4 * j], eA) * d.x;
-        va[b][4 * j + 1] = __builtin_amdgcn_ldexpf(ac[4 * j + 1], eA) * d.y;
-        va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[4 * j + 2], eA) * d.z;
-        va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[4 * j + 3], eA) * d.w;
+      for (int g = 0; g < G; ++g) {
+        const int b = b0 + g;
+        float cm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 d = d2v[b][j];
+          va[b][4 * j] = __builtin_amdgcn_ldexpf(ac[g][4 * j], eA) * d.x;
+          va[b][4 * j + 1] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 1], eA) * d.y;
+          va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 2], eA) * d.z;
+          va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 3], eA) * d.w;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;
+    };
+    using I1 = std::integral_constant<int, 1>;
+    if constexpr (c == 0) {
+      // the phase-B accumulators are still zero constants: room for all four column blocks at once
+      phaseA(std::integral_constant<int, KB_NB>(), std::integral_constant<int, 0>());
+    } else {
+      phaseA(I1(), std::integral_constant<int, 0>());
+      phaseA(I1(), std::integral_constant<int, 1>());
+      phaseA(I1(), std::integral_constant<int, 2>());
+      phaseA(I1(), std::integral_constant<int, 3>());
     }
     __syncthreads();      // column maxima visible; every wave is done reading the previous chunk buffer
     if (c == 0) KSTAMP(2);

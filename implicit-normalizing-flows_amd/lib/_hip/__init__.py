@@ -113,6 +113,7 @@ _SIGS = {
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
     'inf_set_fused_k128': (ctypes.c_int, [ctypes.c_int]),
+    'inf_set_eval_overlap': (ctypes.c_int, [ctypes.c_int]),
     'inf_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int]),
     'inf_net_param_grad': (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t,
                                           _P]),

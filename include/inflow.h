@@ -261,6 +261,14 @@ int inf_debug_poison_lds(void* stream);
  * Returns the previous policy, or -INF_ERR_INVALID for a policy outside 0..2.  No reference counterpart:
  * a performance knob of this build (the reference runs the VJP as autograd, implicit_block.py:418-426). */
 int inf_set_fused_k128(int policy);
+/* Eval schedule of inf_imblock_eval (process-wide): 1 (default, or INFLOW_EVAL_OVERLAP=0 in the environment for 0)
+ * runs the x-branch log-det series on a side stream beside the root solve and the z-branch series (the streams
+ * join before the call returns; needs workspace for a third region, otherwise the call runs sequentially);
+ * 0 runs both series in lockstep on the caller's stream.  Results agree to fp32 roundoff (a per-net launch may
+ * pick another tile variant than the pair's, i.e. another summation order).  Returns the previous value, or
+ * -INF_ERR_INVALID.  No reference counterpart (the reference evaluates the two series one after the other,
+ * implicit_block.py:300-322). */
+int inf_set_eval_overlap(int on);
 
 #ifdef __cplusplus
 }

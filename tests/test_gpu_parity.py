@@ -504,3 +504,32 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B):
         assert torch.isfinite(a).all()
     for a, b in zip(outs[2], outs[0]):
         _close(a, b, rel=1e-5)
+
+
+def test_eval_overlap_matches_sequential():
+    """inf_imblock_eval's overlapped schedule (x-branch series on a side stream beside the root solve and the
+    z-branch series, the default) against the sequential lockstep schedule on the full CIFAR model at B=64 (the
+    bench batch, where the per-net and the paired launches pick different tile variants): same Broyden steps and
+    series lengths, per-sample log p within 2e-3 nats, bits/dim within 1e-5."""
+    arch = syn.CIFAR10
+    B = 64
+    m, _ = _model(arch, B)
+    x = syn.image_batch(B, seed=21).to(DEV)
+    lib = _hip.load()
+    res = {}
+    try:
+        for ov in (1, 0):
+            prev = lib.inf_set_eval_overlap(ov)
+            assert prev in (0, 1)
+            np.random.seed(5)
+            torch.manual_seed(5)
+            bpd, logpx, _ = image_logpx(m, x, arch['nvals'])
+            torch.cuda.synchronize()
+            res[ov] = (bpd.item(), logpx.detach().cpu(), [b.last_broyden['nstep'] for b in imblocks(m)],
+                       [b.last_n_power_series for b in imblocks(m)])
+    finally:
+        lib.inf_set_eval_overlap(1)
+    assert lib.inf_set_eval_overlap(2) < 0
+    assert res[1][2] == res[0][2] and res[1][3] == res[0][3]
+    assert abs(res[1][0] - res[0][0]) <= 1e-5
+    np.testing.assert_allclose(res[1][1].numpy(), res[0][1].numpy(), rtol=0, atol=2e-3)

@@ -26,6 +26,11 @@ def main():
     ap.add_argument('write_dir')
     ap.add_argument('--batch', type=int, default=64)
     ap.add_argument('--out', default='profiles/pmc_dominant_kernel.json')
+    # the dominant kernel: the 128-pixel K-chunked VJP (tag 532); the 64-pixel one is
+    # --prefix 'void inf::net313_kernel<2, 2' --tag 502 --kernel 'net313_kernel<VJP>'
+    ap.add_argument('--prefix', default='inf::net313k_vjp_kernel')
+    ap.add_argument('--tag', type=int, default=532)
+    ap.add_argument('--kernel', default='net313k_kernel<VJP>')
     a = ap.parse_args()
     f, w = load(a.fetch_dir, 'FETCH_SIZE'), load(a.write_dir, 'WRITE_SIZE')
     rows, vjp = [], []
@@ -35,9 +40,9 @@ def main():
         hbm = 2 * fetch + write
         rows.append({'kernel': k[0], 'grid_threads': k[1], 'dispatches': len(f[k]), 'fetch_size_bytes': fetch,
                      'write_size_bytes': write, 'hbm_bytes_corrected': hbm})
-        if k[0].startswith('void inf::net313_kernel<2, 2'):   # tag 502 (64-pixel tiles, any MFMA mode); _h is tag 512
+        if k[0].startswith(a.prefix):
             vjp += [hbm] * len(f[k])
-    res = {'tag': 502, 'kernel': 'net313_kernel<VJP>', 'batch': a.batch,
+    res = {'tag': a.tag, 'kernel': a.kernel, 'batch': a.batch,
            'hbm_bytes_per_launch': sum(vjp) / len(vjp) if vjp else None,
            'method': '2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch, separate --pmc passes, averaged over the '
                      'net313_kernel<2, 2> (64-pixel-tile VJP) dispatches of the bench run', 'per_config': rows}
