@@ -1120,8 +1120,8 @@ static void timing_collect(const char* key, long nwg, hipStream_t s) {
   }
 }
 
-// VJP variant policy (inf_set_fused_k128): 0 the 64-pixel kernel only, 1 the 128-pixel K-chunked kernel where its
-// grid still covers every CU (default; INFLOW_FUSED_K128 in the environment), 2 wherever it fits (tests)
+// VJP / EVAL variant policy (inf_set_fused_k128): 0 the 64-pixel kernel only, 1 the 128-pixel K-chunked kernel where
+// its grid still covers every CU (default; INFLOW_FUSED_K128 in the environment), 2 wherever it fits (tests)
 static std::atomic<int> g_k128{[] {
   const char* e = getenv("INFLOW_FUSED_K128");
   return e ? atoi(e) : 1;
@@ -1163,7 +1163,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // 128-pixel K-chunked VJP (fused313k.hip): h3 (all phases), where the pair's derivatives are in the 64-pixel
   // layout and the grid still covers every CU
   const int k128_pol = g_k128.load(std::memory_order_relaxed);
-  const bool k128 = k128_pol && H3_AC && h3_args && mode == MODE_VJP && var == V64 && force_bn == 0 &&
+  const bool k128 = k128_pol && H3_AC && h3_args && (mode == MODE_VJP || mode == MODE_EVAL) && var == V64 && force_bn == 0 &&
                     force_var < 0 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
                     (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
   const int tbn = k128 ? 128 : bn;
@@ -1198,7 +1198,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
   if (k128) {
-    INF_TRY(launch_net313k_vjp(pr, nb, s));
+    INF_TRY(launch_net313k(pr, mode, nb, s));
     if (pr.tbuf) {
       char key[64];
       snprintf(key, sizeof(key), "var3 mode%d split2 C%d", mode, a0.C);
@@ -1207,8 +1207,8 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     if (prof) {
       const double npx = (double)nnets * a0.B * P;
       const double f = 2.0 * hid * 9.0 * a0.C * 2.0 + 2.0 * hid * hid;
-      const double bytes = 4.0 * npx * (a0.C + 2.0 * hid + 9.0 * a0.C);
-      prof_end_launch(s, 532, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+      const double bytes = 4.0 * npx * (a0.C + (mode == MODE_VJP ? 2.0 * hid : 0.0) + 9.0 * a0.C);
+      prof_end_launch(s, 530 + mode, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
     }
     return INF_OK;
   }

@@ -70,7 +70,10 @@ int net313k_fits(int hid, int C, int H, int W) {
   return need <= KB_LDS;
 }
 
-__global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
+// MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2))
+template <int MODE>
+__global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
+  constexpr bool VJP = MODE == MODE_VJP;
   const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
   const Net313Args& a = pr.a[sel];
   const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
   auto loadD2 = [&](int c, int b0, int b1) {
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
-      if (b < b0 || b >= b1) continue;
+      if (!VJP || b < b0 || b >= b1) continue;
       const f32x4* q = dptr(a.d2, 8 * c + wid, b);
 #pragma unroll
       for (int j = 0; j < 4; ++j) d2v[b][j] = q[j];
@@ -252,6 +255,7 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
   const u32x4* A3h = reinterpret_cast<const u32x4*>(a.A3h);
   const int nkt1 = a.K1pad / 16;
   const int ew = a.Ah_exp[1];
+  const float sp1 = VJP ? 0.f : softplus_f(*a.beta1), sp2 = VJP ? 0.f : softplus_f(*a.beta2);
 
   // writes this wave's values of one 32-row block (rows kt0 * 16 .. + 31 of the chunk) and column block b
   // into the chunk buffer: accumulator group g holds rows 8g + 4 lh + q, which consumer lane 32 (g & 1) + li
@@ -325,11 +329,19 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
         float cm = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const f32x4 d = d2v[b][j];
-          va[b][4 * j] = __builtin_amdgcn_ldexpf(ac[g][4 * j], eA) * d.x;
-          va[b][4 * j + 1] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 1], eA) * d.y;
-          va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 2], eA) * d.z;
-          va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 3], eA) * d.w;
+          if constexpr (VJP) {
+            const f32x4 d = d2v[b][j];
+            va[b][4 * j] = __builtin_amdgcn_ldexpf(ac[g][4 * j], eA) * d.x;
+            va[b][4 * j + 1] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 1], eA) * d.y;
+            va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 2], eA) * d.z;
+            va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 3], eA) * d.w;
+          } else {                                   // forward: swish(a1 + b1), rows of accumulator group j
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int row = rbA * 32 + q + 8 * j + 4 * lh;
+              va[b][4 * j + q] = swish_f(__builtin_amdgcn_ldexpf(ac[g][4 * j + q], eA) + a.b1[row], sp1);
+            }
+          }
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
@@ -421,6 +433,7 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
     f32x4 d1v[KB_NB][4];
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
+      if constexpr (!VJP) break;
       const f32x4* q = dptr(a.d1, 2 * wid + m, b);
 #pragma unroll
       for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];
@@ -428,6 +441,15 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
       const int e = -(scB[b] + ew);
+      if constexpr (!VJP) {                        // forward: swish(a2 + b2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (2 * wid + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          acc[m][b][r] = swish_f(__builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row], sp2);
+          cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 d = d1v[b][j];
@@ -553,8 +575,10 @@ __global__ __launch_bounds__(512) void net313k_vjp_kernel(Net313Pair pr) {
 #undef KSTAMP
 }
 
-int launch_net313k_vjp(const Net313Pair& pr, unsigned nb, hipStream_t s) {
-  hipLaunchKernelGGL(net313k_vjp_kernel, dim3(nb), dim3(KB_NT), 0, s, pr);
+int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s) {
+  if (mode == MODE_VJP) hipLaunchKernelGGL(net313k_kernel<MODE_VJP>, dim3(nb), dim3(KB_NT), 0, s, pr);
+  else if (mode == MODE_EVAL) hipLaunchKernelGGL(net313k_kernel<MODE_EVAL>, dim3(nb), dim3(KB_NT), 0, s, pr);
+  else return INF_ERR_UNSUPPORTED;
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

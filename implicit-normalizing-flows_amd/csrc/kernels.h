@@ -177,9 +177,9 @@ struct Net313Pair {
                           // d1 load, 2 skip the d2 load, 4 skip phase C, 8 skip the input staging
 };
 int net313_supported(int hid, int C, int H, int W);
-// 128-pixel K-chunked VJP variant (fused313k.hip, INF_MFMA_F16X3 only)
+// 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
 int net313k_fits(int hid, int C, int H, int W);
-int launch_net313k_vjp(const Net313Pair& pr, unsigned nb, hipStream_t s);
+int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s);
 int set_fused_k128(int policy);   // returns the previous policy, -1 for an invalid one
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 // layout_nets (> 0) picks the tile variant as if that many nets shared the grid: launches that write

@@ -254,12 +254,13 @@ int inf_net_surrogate_grad(InfNet* net, const float* x, const float* w, const fl
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);
-/* Which kernel runs the fused VJP of 512-wide nets in INF_MFMA_F16X3 (process-wide; fused313k.hip):
+/* Which kernel runs the fused VJP and forward (EVAL) of 512-wide nets in INF_MFMA_F16X3 (process-wide; fused313k.hip):
  *   0  the 64-pixel kernel only;
  *   1  the 128-pixel K-chunked kernel where its grid still covers all 256 CUs (default, or INFLOW_FUSED_K128);
  *   2  the 128-pixel kernel wherever its tile fits (parity tests at small batch).
  * Returns the previous policy, or -INF_ERR_INVALID for a policy outside 0..2.  No reference counterpart:
- * a performance knob of this build (the reference runs the VJP as autograd, implicit_block.py:418-426). */
+ * a performance knob of this build (the reference runs the VJP as autograd, implicit_block.py:418-426, and the
+ * forward as three F.conv2d calls, mixed_lipschitz.py:388-391). */
 int inf_set_fused_k128(int policy);
 /* Eval schedule of inf_imblock_eval (process-wide): 1 (default, or INFLOW_EVAL_OVERLAP=0 in the environment for 0)
  * runs the x-branch log-det series on a side stream beside the root solve and the z-branch series (the streams

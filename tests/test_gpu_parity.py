@@ -453,8 +453,8 @@ def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3])
 def test_fused_k128_vjp_matches_64px_kernel(block, B):
-    """The 128-pixel K-chunked VJP (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
-    256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net VJP, the chained log-det
+    """The 128-pixel K-chunked kernel (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
+    256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net forward, the VJP, the chained log-det
     series (each term stages the previous term's taps, preact swish' and trace partial) and the Neumann vector
     (each term stages the accumulation w += c_k v_k), with the workspace and every CU's LDS NaN-poisoned before
     each call.  inf_set_fused_k128(2) forces the 128-pixel kernel at these small grids.  Tolerance: 1e-5 of
@@ -485,7 +485,10 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B):
         for pol in (2, 0):
             prev = net.lib.inf_set_fused_k128(pol)
             assert prev in (0, 1, 2)
-            g, ld, w = torch.empty_like(x), torch.empty(B, device=DEV), torch.empty_like(x)
+            y, g, ld, w = torch.empty_like(x), torch.empty_like(x), torch.empty(B, device=DEV), torch.empty_like(x)
+            poison()
+            _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
+                                               stream), 'fwd')
             poison()
             _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(x), _hip.ptr(v), _hip.ptr(g), B, _hip.ptr(ws),
                                            ws.numel(), stream), 'vjp')
@@ -496,7 +499,7 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B):
             _hip.check(net.lib.inf_neumann_vector(net.handle, _hip.ptr(x), _hip.ptr(eps), fptr(nco), n, _hip.ptr(w), B,
                                                   _hip.ptr(ws), ws.numel(), stream), 'neumann')
             torch.cuda.synchronize()
-            outs[pol] = (g, ld, w)
+            outs[pol] = (y, g, ld, w)
     finally:
         net.lib.inf_set_fused_k128(1)
     assert net.lib.inf_set_fused_k128(3) < 0
