@@ -36,6 +36,23 @@ def test_binding_signatures_cover_header():
     assert set(_declared_symbols()) == set(_hip.EXPORTS)
 
 
+def test_process_wide_schedule_switches():
+    """inf_set_fused_k128 (0 / 1 / 2) and inf_set_eval_overlap (0 / 1) return the previous value and reject
+    anything else with -INF_ERR_INVALID, leaving the setting unchanged (host-only: no GPU call)."""
+    if not os.path.exists(_hip.LIB_PATH):
+        pytest.skip('libinflow.so not built (run __graft_entry__.build())')
+    lib = _hip.load()
+    k0 = lib.inf_set_fused_k128(2)
+    assert k0 in (0, 1, 2)
+    assert lib.inf_set_fused_k128(7) == -1 and lib.inf_set_fused_k128(-1) == -1
+    assert lib.inf_set_fused_k128(0) == 2
+    assert lib.inf_set_fused_k128(k0) == 0
+    o0 = lib.inf_set_eval_overlap(0)
+    assert o0 in (0, 1)
+    assert lib.inf_set_eval_overlap(2) == -1
+    assert lib.inf_set_eval_overlap(o0) == 0
+
+
 @pytest.mark.parametrize('dist,param,n_exact', [('poisson', 2.0, 20), ('geometric', 0.5, 2), ('poisson', 2.0, 10)])
 def test_series_coefficients_match_oracle(dist, param, n_exact):
     np.random.seed(123)
