@@ -29,6 +29,17 @@ __device__ __forceinline__ float swish_d(float a, float sp) {
   return (s + (a * s) * (1.f - s) * sp) / 1.1f;
 }
 
+// Fast forms for the fused 3-1-3 kernels' per-element epilogues (fused313.hip, fused313k.hip), where the precise forms'
+// two IEEE divisions and range-reduced expf were most of the VALU of the EVAL / SAVE launches: v_exp_f32 and
+// v_rcp_f32 (relative error of sigmoid <= ~1e-6 for |a sp| <= 16, against the fused kernels' 1e-5 parity bound), the
+// division by 1.1 as a multiply.  The generic GEMM path, conv_out and the gradients keep the precise forms.
+__device__ __forceinline__ float sigmoid_fast(float z) { return __frcp_rn(1.f + __expf(-z)); }
+__device__ __forceinline__ float swish_fast_f(float a, float sp) { return a * sigmoid_fast(a * sp) * (1.f / 1.1f); }
+__device__ __forceinline__ float swish_fast_d(float a, float sp) {
+  const float s = sigmoid_fast(a * sp);
+  return (s + (a * s) * (1.f - s) * sp) * (1.f / 1.1f);
+}
+
 constexpr float TWO_PI_F = 6.283185307179586f;
 constexpr float PI_F = 3.141592653589793f;
 

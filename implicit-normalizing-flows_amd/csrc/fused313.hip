@@ -212,7 +212,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
           v += vt ? tv[u][tp] : 0.f;
         }
-        if (mx) v = v * swish_d(xm[u], msp);
+        if (mx) v = v * swish_fast_d(xm[u], msp);
         v = ok ? v : 0.f;
         if (ep && ok == 2) dacc += (double)v * (double)ev[u];
         if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
@@ -237,7 +237,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
         if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
           v = in[(long)c * P + yy * a.W + xx];
-          if (a.pre_beta) v = swish_f(v, pre_sp);
+          if (a.pre_beta) v = swish_fast_f(v, pre_sp);
         }
       }
       if constexpr (H3AC) hmx = fmaxf(hmx, fabsf(v));
@@ -480,8 +480,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             v = acc[m][b][r] * dmul[m][b][r];
           } else {
             const float z = acc[m][b][r] + a.b1[o];
-            v = swish_f(z, sp1);
-            if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) dv[r] = swish_d(z, sp1);
+            v = swish_fast_f(z, sp1);
+            if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) dv[r] = swish_fast_d(z, sp1);
           }
           if constexpr (H3) cm[b] = fmaxf(cm[b], fabsf(v));
           t[o * F_BN + b * 32 + li] = v;
@@ -716,7 +716,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int b = 0; b < NB; ++b) {
         float dv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dv[r] = swish_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
+        for (int r = 0; r < 16; ++r) dv[r] = swish_fast_d(acc[m][b][r] + a.b2[row_of(m, r)], sp2);
         store_d(a.d2, m, b, dv);
       }
   }
@@ -742,7 +742,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         for (int r = 0; r < 16; ++r) {
           const int o = row_of(m, r);
           if constexpr (MODE == MODE_VJP) acc[m][b][r] = acc[m][b][r] * dmul[m][b][r];
-          else acc[m][b][r] = swish_f(acc[m][b][r] + a.b2[o], sp2);
+          else acc[m][b][r] = swish_fast_f(acc[m][b][r] + a.b2[o], sp2);
         }
     if (pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
       float s_ = 0.f;

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
             const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
             v += vt ? tv[u][tp] : 0.f;
           }
-          if (mx) v = v * swish_d(xm[u], msp);
+          if (mx) v = v * swish_fast_d(xm[u], msp);
           v = ok ? v : 0.f;
           if (ep && ok == 2) dacc += (double)v * (double)ev[u];
           if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           const int yy = y0 + hy - 1, xx = x0 + hx - 1;
           if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
             v = in[(long)c * P + yy * a.W + xx];
-            if (a.pre_beta) v = swish_f(v, pre_sp);
+            if (a.pre_beta) v = swish_fast_f(v, pre_sp);
           }
         }
         hmx = fmaxf(hmx, fabsf(v));
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int row = rbA * 32 + q + 8 * j + 4 * lh;
-              va[b][4 * j + q] = swish_f(__builtin_amdgcn_ldexpf(ac[g][4 * j + q], eA) + a.b1[row], sp1);
+              va[b][4 * j + q] = swish_fast_f(__builtin_amdgcn_ldexpf(ac[g][4 * j + q], eA) + a.b1[row], sp1);
             }
           }
         }
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = (2 * wid + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          acc[m][b][r] = swish_f(__builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row], sp2);
+          acc[m][b][r] = swish_fast_f(__builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row], sp2);
           cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
         }
         continue;
