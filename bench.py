@@ -16,6 +16,7 @@ Prints one JSON line on rank 0 (metric, value = samples/s over all ranks, roofli
 dominant kernel measured live with HIP events, cpu_baseline = the oracle on the host cores).
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -32,9 +33,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from lib import _hip, distributed as dd, synthetic as syn  # noqa: E402
-from lib.configs import build_flow, imblocks  # noqa: E402
+from lib.configs import build_flow, imblocks, restore_engine_options, set_engine_option  # noqa: E402
 from lib.density import image_bits_per_dim_graph, image_logpx  # noqa: E402
-from lib.layers import set_probe_mode  # noqa: E402
+from lib.layers import set_probe_mode, set_probe_shard  # noqa: E402
 
 METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs are labelled alike
     'cifar10': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 density eval at 1/8 GPU',
@@ -46,9 +47,22 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA peak (102
 
 
 def mfma_mode():
-    """Arithmetic of the fused kernels, as inf_net_create picks it (engine.hip: INFLOW_MFMA=f32 / bf16x6 / f16x3)."""
+    """Arithmetic of the fused kernels, as inf_net_create picks it (engine.hip: INFLOW_MFMA=f32 / fp32 / bf16x6 /
+    f16x3, anything else is rejected there)."""
     e = os.environ.get('INFLOW_MFMA', '')
-    return 'f32' if e.startswith('f3') else ('bf16x6' if e.startswith('b') else 'f16x3')
+    return 'f32' if e in ('f32', 'fp32') else ('bf16x6' if e == 'bf16x6' else 'f16x3')
+
+
+KERNEL_SOURCES = ('fused313k.hip', 'fused313.hip', 'common.h', 'kernels.h')
+
+
+def kernel_source_sha():
+    """Hash of the fused-kernel sources: a committed PMC traffic record counts only for the build it was measured on."""
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(PKG, 'csrc', f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 MFMA_DESC = {
@@ -71,7 +85,8 @@ def parse():
     ap.add_argument('--config', default='cifar10', choices=['cifar10', 'cifar10_small', 'celebahq256'])
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
-    ap.add_argument('--cpu-batch', type=int, default=16, help='images in the bounded CPU-baseline sample (~10-15 s)')
+    ap.add_argument('--cpu-batch', type=int, default=8,
+                    help='images per timed CPU-baseline batch (1 warm-up batch of half that, then the median of 3)')
     ap.add_argument('--train-step', default='full', choices=['full', 'fwdbwd'],
                     help='train mode: full = forward + backward + clip_grad_norm_(1) + Adam + update_lipschitz + '
                          'EMA (train_img.py:637-658); fwdbwd = forward + backward only')
@@ -82,27 +97,37 @@ def parse():
 
 
 def cpu_baseline(arch, sd, model, device, nimg):
-    """Oracle (CPU restatement, torch fp32, autograd VJPs) on a bounded sample; also the GPU path on
-    the same sample with the reference RNG replay -> |bpd_gpu - bpd_oracle|."""
+    """Oracle (CPU restatement, torch fp32, autograd VJPs) timed as BASELINE.md's CPU-baseline plan prescribes --
+    one warm-up batch, then the median of 3 batches -- on batches of `nimg` images (bounded: B=64 batches would take
+    minutes of CPU per batch); also the GPU path on the last batch with the reference RNG replay ->
+    |bpd_gpu - bpd_oracle|."""
     from oracle import inflow_oracle as orc
     cores = max(1, min(int(os.environ.get('OMP_NUM_THREADS', '16')), os.cpu_count() or 1))
     torch.set_num_threads(cores)
-    x = syn.image_batch(nimg, arch['input_size'], arch['nvals'], seed=777)
     flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
-    np.random.seed(11)
-    torch.manual_seed(11)
-    t0 = time.perf_counter()
-    ref_bpd, _, _ = orc.image_bits_per_dim(flow, x, arch['nvals'])
-    dt = time.perf_counter() - t0
+    xw = syn.image_batch(max(1, nimg // 2), arch['input_size'], arch['nvals'], seed=776)
+    np.random.seed(10)
+    torch.manual_seed(10)
+    orc.image_bits_per_dim(flow, xw, arch['nvals'])            # warm-up batch (untimed)
+    times = []
+    for r in range(3):
+        x = syn.image_batch(nimg, arch['input_size'], arch['nvals'], seed=777 + r)
+        np.random.seed(11 + r)
+        torch.manual_seed(11 + r)
+        t0 = time.perf_counter()
+        ref_bpd, _, _ = orc.image_bits_per_dim(flow, x, arch['nvals'])
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     set_probe_mode('reference')
-    np.random.seed(11)
-    torch.manual_seed(11)
+    np.random.seed(11 + 2)
+    torch.manual_seed(11 + 2)
     gpu_bpd, _, _ = image_logpx(model, x.to(device), arch['nvals'])
     torch.cuda.synchronize()
-    set_probe_mode('device')
+    set_probe_mode('device', seed=12345)
     return ({'value': nimg / dt, 'unit': 'samples/s', 'cores': cores, 'kind': 'port',
-             'sample': '%d CIFAR-shaped images through the full %s model (oracle/inflow_oracle.py, torch fp32 '
-                       'CPU, %d threads), %.1f s' % (nimg, 'run_cifar10.sh', cores, dt)},
+             'sample': 'oracle/inflow_oracle.py (torch fp32 CPU, %d threads) on the full run_cifar10.sh model: one '
+                       'warm-up batch of %d images, then the median of 3 batches of %d CIFAR-shaped images '
+                       '(%.1f / %.1f / %.1f s)' % (cores, max(1, nimg // 2), nimg, *times)},
             abs(float(gpu_bpd) - float(ref_bpd)), float(ref_bpd))
 
 
@@ -121,7 +146,11 @@ def main():
     xs = torch.stack([syn.image_batch(B, arch['input_size'], arch['nvals'], seed=1000 * rank + i)
                       for i in range(min(nsteps, 4))]).to(device)
     ndim = int(np.prod(arch['input_size']))
-    set_probe_mode(args.probes, seed=12345 + rank)
+    # probes in the global reference order, each rank keeping its rows: the same probes per sample
+    # as a single-process run over the world * B batch
+    set_probe_mode(args.probes, seed=12345)
+    if world > 1:
+        set_probe_shard(rank * B, (rank + 1) * B, world * B)
     np.random.seed(0)
     torch.manual_seed(0)
 
@@ -171,15 +200,15 @@ def main():
     # this step runs the sequential one, so each kernel's HIP-event duration is its own, not shared with a
     # concurrent launch (tools/profile_round.sh runs rocprofv3 with INFLOW_EVAL_OVERLAP=0 to match).
     steps_info = [b.last_broyden['nstep'] for b in imblocks(model)]
-    lib = _hip.load()
-    overlap_prev = lib.inf_set_eval_overlap(0)
+    overlap_prev = set_engine_option(model, _hip.INF_OPT_EVAL_OVERLAP, 0)
+    overlap_on = any(v == 1 for v in overlap_prev.values())
     _hip.profile_begin(100000)
     t1 = time.perf_counter()
     step(0)
     torch.cuda.synchronize()
     prof_wall = time.perf_counter() - t1
     stats = _hip.profile_end()
-    lib.inf_set_eval_overlap(overlap_prev)
+    restore_engine_options(_hip.INF_OPT_EVAL_OVERLAP, overlap_prev)
     nps = [getattr(b, 'last_n_power_series', None) for b in imblocks(model)]
     gemms = [s for s in stats if s['flops'] > 0]          # MFMA kernels (GEMM family + fused net)
     dom = max(gemms, key=lambda s: s['total_ms'])
@@ -187,13 +216,18 @@ def main():
     achieved = dom['flops'] / dom['launches'] / (avg_ms * 1e-3) / 1e12
     total_gemm_flops = sum(s['flops'] for s in gemms)
     total_kernel_ms = sum(s['total_ms'] for s in stats)
-    traffic = None
+    # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes (tools/pmc_summary.py:
+    # 2 FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), counted only when they were measured on
+    # this kernel, batch, schedule and kernel-source build
+    traffic, traffic_src = None, None
     pmc_path = os.path.join(REPO, 'profiles', 'pmc_dominant_kernel.json')
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            if pmc.get('tag') == dom['tag'] and pmc.get('batch') == B:
+            if (pmc.get('tag') == dom['tag'] and pmc.get('batch') == B and args.config == pmc.get('config', 'cifar10')
+                    and pmc.get('kernel_source_sha') == kernel_source_sha()):
                 traffic = pmc.get('hbm_bytes_per_launch')
+                traffic_src = 'profiles/pmc_dominant_kernel.json (%s)' % pmc.get('measured', '?')
         except Exception:
             traffic = None
 
@@ -227,9 +261,10 @@ def main():
                                     '3 in f16x3 phases; f32 %.1f TF)' % (BF16_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS)),
                      'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not MFMA instruction FLOPs',
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
+                     'traffic_source': traffic_src,
+                     'algorithmic_bytes_per_launch': dom['bytes'] / dom['launches'],
                      'schedule': 'per-kernel durations from one extra step on the sequential eval schedule (timed '
-                                 'steps: %s)' % ('x-branch series on a side stream' if overlap_prev == 1
-                                                else 'sequential'),
+                                 'steps: %s)' % ('x-branch series on a side stream' if overlap_on else 'sequential'),
                      'flops_per_launch': dom['flops'] / dom['launches']},
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),
                  'gemm_flop_rate_tflops': round(total_gemm_flops / (prof_wall * 1e12), 2),

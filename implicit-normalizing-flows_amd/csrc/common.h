@@ -143,10 +143,12 @@ __device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4& h, c
 }
 
 // ---- scaled two-piece fp16 ("h3") contraction: phase B of INF_MFMA_F16X3 (include/inflow.h) ----------
-// x*S = h + l + e with h = rne16(x*S), l = rne16(x*S - h) (x*S - h is exact in fp32), |e| <= 2^-24 |x*S|
-// while l stays a normal fp16, i.e. for |x*S| >= 2^-2.  S = 2^s puts a column's (or matrix's) max in
-// [2^14, 2^15): below max*2^-16 the pieces lose precision only in absolute terms <= max*2^-39.  Products
-// hh + hl + lh on v_mfma_f32_32x32x16_f16 (exact 22-bit products, fp32 accumulation); ll <= 2^-24 |x||w|.
+// x*S = h + l + e with h = rne16(x*S), l = rne16(x*S - h) (x*S - h is exact in fp32): |x*S - h| <= 2^-12 |x*S|
+// rounded to 11 bits again, so |e| <= 2^-23 |x*S| while l stays a normal fp16 (|x*S - h| >= 2^-14); below that l
+// is subnormal and |e| <= 2^-25 absolute.  S = 2^s puts the set's (column's, tile's, matrix's) max m in
+// [2^14, 2^15), so the bound relative to the set is |e| <= 2^-23 m*S for every element: small entries get an
+// absolute, not a relative, bound.  Products hh + hl + lh on v_mfma_f32_32x32x16_f16 (exact 22-bit products,
+// fp32 accumulation); the dropped ll is <= 2^-24 |x||w|.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // scale exponent s for a set whose max |x| is m: m * 2^s in [2^14, 2^15); 0 for m == 0 / inf / NaN
@@ -155,7 +157,7 @@ __host__ __device__ __forceinline__ int h3_scale_exp(float m) {
   int e;
   (void)frexpf(m, &e);            // m = f 2^e, f in [0.5, 1)
   const int s = 15 - e;
-  return s < -100 ? -100 : (s > 100 ? 100 : s);
+  return s < -140 ? -140 : (s > 140 ? 140 : s);   // any finite fp32 max maps into [2^14, 2^15) (no fp16 overflow)
 }
 __device__ __forceinline__ void split2h(const float (&x)[8], float S, u32x4& h, u32x4& l) {
 #pragma unroll

@@ -11,13 +11,16 @@
 //   inf_logdet_neumann    <- neumann_logdet_estimator                                    (:429-438)
 //   inf_logdet_exact      <- brute-force batch_jacobian + torch.logdet                   (:249-260)
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
 #include <new>
+#include <chrono>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "glue.h"
@@ -27,15 +30,15 @@ namespace inf {
 static thread_local int g_last_hip = 0;
 void set_hip_error(hipError_t e) { g_last_hip = (int)e; }
 
-// ---- opt-in launch timing -------------------------------------------------------------------
+// ---- opt-in launch timing (per host thread: a profile session records the launches its own thread makes) ----
 struct ProfSlot {
   hipEvent_t a, b;
   int tag;
   double flops, bytes, peak_ms;
 };
-static std::vector<ProfSlot> g_prof;
-static size_t g_prof_used = 0;
-static bool g_prof_on = false;
+static thread_local std::vector<ProfSlot> g_prof;
+static thread_local size_t g_prof_used = 0;
+static thread_local bool g_prof_on = false;
 bool prof_enabled() { return g_prof_on && g_prof_used < g_prof.size(); }
 void prof_begin_launch(hipStream_t s) { (void)hipEventRecord(g_prof[g_prof_used].a, s); }
 void prof_end_launch(hipStream_t s, int tag, double flops, double bytes, double peak_ms) {
@@ -104,6 +107,10 @@ struct InfNet {
   // Broyden residual; computed by a launch of the same batch size (same tile variant -> same bits)
   float* f0 = nullptr;
   int f0_batch = -1;
+  // per-net options (inf_net_set_option; defaults from the environment at inf_net_create)
+  int k128 = 1;            // INF_OPT_FUSED_K128
+  int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
+  int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
 };
 
 namespace {
@@ -133,7 +140,11 @@ struct Bufs {
   float* fspec;            // root solve: f(z) of the speculative iteration in flight (broyden_core)
   float *U, *VT;
   float *ext0, *ext1;
-  double *part, *bpart, *sumsq;
+  double *part, *bpart, *sumsq;   // sumsq: B per-sample sums of squares + 1 (per-sample mode: samples iterating)
+  // per-sample convergence (INF_CONV_PER_SAMPLE): state machine, flags, lowest iterate and its f
+  double* ps_state;
+  int *ps_active, *ps_improved;
+  float *ps_lowx, *ps_lowf;
   unsigned int* counter;
   int nchunk;              // per-sample partial chunks of conv_out (residual norms, unfused series)
   float* Y2;               // fused nets: second taps buffer (series terms alternate Y / Y2)
@@ -161,7 +172,7 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   for (auto& p : b.D) p = w.take<float>(Hs);
   float** vecs[] = {&b.xin, &b.xemb, &b.fx, &b.xa, &b.xb, &b.ga, &b.gb, &b.upd,
                     &b.dx, &b.dg, &b.lowest, &b.va, &b.vb, &b.eps_t, &b.zero, &b.tmp, &b.fcur, &b.flow,
-                    &b.fspec};
+                    &b.fspec, &b.ps_lowx, &b.ps_lowf};
   for (float** v : vecs) *v = w.take<float>(E);
   b.U = w.take<float>((size_t)T * E);
   b.VT = w.take<float>((size_t)T * E);
@@ -175,8 +186,11 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   b.part = w.take<double>((size_t)B * std::max(nchunk, b.snchunk) * SERIES_MAX);
   const int bch = (n->d + 1023) / 1024;
   b.bpart = w.take<double>((size_t)B * bch * (3 * (size_t)T + 2) + 64);
-  b.sumsq = w.take<double>((size_t)B);
+  b.sumsq = w.take<double>((size_t)B + 1);
   b.counter = w.take<unsigned int>(64);
+  b.ps_state = w.take<double>((size_t)B * (PS_HEAD + T));
+  b.ps_active = w.take<int>((size_t)B);
+  b.ps_improved = w.take<int>((size_t)B);
   return w.off + 256;
 }
 
@@ -252,6 +266,7 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.H = n->H;
   f.W = n->W;
   f.seg = n->W < 64 ? n->W : 64;
+  f.k128 = n->k128;
   return f;
 }
 
@@ -381,10 +396,10 @@ struct SumsSlot {
 static int sums_slot(int i, int B, SumsSlot** out) {
   static thread_local SumsSlot slots[2];
   SumsSlot& sl = slots[i & 1];
-  if (sl.cap < B) {
+  if (sl.cap < B + 1) {
     if (sl.host) (void)hipHostFree(sl.host);
     sl.host = nullptr;
-    const int cap = std::max(B, 1024);
+    const int cap = std::max(B + 1, 1024);
     if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sizeof(double) * cap, hipHostMallocDefault) != hipSuccess)
       return INF_ERR_HIP;
     sl.cap = cap;
@@ -393,20 +408,34 @@ static int sums_slot(int i, int B, SumsSlot** out) {
   *out = &sl;
   return INF_OK;
 }
-int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
-  if (f->fc) {
-    INF_HIP(hipMemcpyAsync(sl->host, bf.part, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-  } else {
-    INF_TRY(launch_reduce_partials(bf.part, B, bf.nchunk, bf.sumsq, s));
-    INF_HIP(hipMemcpyAsync(sl->host, bf.sumsq, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+// The per-sample stopping decision of step k (INF_CONV_PER_SAMPLE), queued between the reduction and the
+// readback: the device state machine (pointwise.hip ps_decide_kernel) and the copy of the improved samples'
+// iterate (and f) into the lowest-iterate buffers.  The readback then carries the count of samples iterating.
+struct PsStep {
+  bool on = false;
+  int k = 0, T = 0;
+  double eps = 0.0;          // eps * sqrt(d)
+  const float* x = nullptr;  // the iterate of this residual
+  const float* f = nullptr;  // its f (nullable)
+  long sb = 0, si = 0;
+};
+int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const PsStep* ps = nullptr) {
+  INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, bf.sumsq, s));
+  int n = B;
+  if (ps && ps->on) {
+    INF_TRY(launch_ps_decide(bf.sumsq, bf.ps_state, bf.ps_active, bf.ps_improved, B, ps->k, ps->T, ps->eps, s));
+    INF_TRY(launch_ps_copy(bf.ps_improved, ps->x, ps->f, bf.ps_lowx, bf.ps_lowf, B, f->d, ps->sb, ps->si, s));
+    n = B + 1;
   }
+  INF_HIP(hipMemcpyAsync(sl->host, bf.sumsq, sizeof(double) * n, hipMemcpyDeviceToHost, s));
   INF_HIP(hipEventRecord(sl->ev, s));
   return INF_OK;
 }
 // Host wait on a readback event.  A blocking hipEventSynchronize that has to wait long (e.g. behind a whole
 // log-det series) lets the runtime put the thread to sleep, and its wake-up comes late, with the GPU idle
-// and nothing else queued; polling hipEventQuery keeps the host turnaround at the copy's latency.
-// INFLOW_BLOCKING_WAIT=1 restores the blocking wait.
+// and nothing else queued; polling hipEventQuery keeps the host turnaround at the copy's latency.  The poll
+// spins for at most 100 us, then yields the core between polls (other host threads, e.g. data loaders, run),
+// and after 5 ms sleeps 20 us per poll.  INFLOW_BLOCKING_WAIT=1 restores the blocking wait.
 int host_wait(hipEvent_t ev) {
   static const bool blocking = [] {
     const char* e = getenv("INFLOW_BLOCKING_WAIT");
@@ -416,6 +445,7 @@ int host_wait(hipEvent_t ev) {
     INF_HIP(hipEventSynchronize(ev));
     return INF_OK;
   }
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return INF_OK;
@@ -423,11 +453,16 @@ int host_wait(hipEvent_t ev) {
       set_hip_error(q);
       return INF_ERR_HIP;
     }
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (us > 5000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else if (us > 100) std::this_thread::yield();
   }
 }
-int wait_sumsq(SumsSlot* sl, int B, std::vector<double>& host_sumsq) {
+// n_active (may be null): the per-sample mode's count of samples still iterating after this step
+int wait_sumsq(SumsSlot* sl, int B, std::vector<double>& host_sumsq, int* n_active = nullptr) {
   INF_TRY(host_wait(sl->ev));
   memcpy(host_sumsq.data(), sl->host, sizeof(double) * B);
+  if (n_active) *n_active = (int)sl->host[B];
   return INF_OK;
 }
 int read_sumsq(InfNet* f, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
@@ -437,45 +472,34 @@ int read_sumsq(InfNet* f, int B, Bufs& bf, std::vector<double>& host_sumsq, hipS
   return wait_sumsq(sl, B, host_sumsq);
 }
 
-// residual evaluation g = x_embed - f(z) - z (+ dg = g - g_prev) and per-sample sum of squares -> host
-// zsub is the subtracted "- z" term: z itself for Broyden, zeros for the Banach map x_embed - f(z).
+// residual evaluation g = x_embed - f(z) - z (+ dg = g - g_prev), f(z) kept in bf.fcur, per-sample partial sums of
+// squares in bf.part.  zsub is the subtracted "- z" term: z itself for Broyden, zeros for the Banach map.
+int eval_resid_part(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
+                    const float* gprev, int B, Bufs& bf, hipStream_t s) {
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = xemb;
+  a.in1 = zsub;
+  a.in2 = gprev;
+  a.out0 = gout;
+  a.out1 = dg;
+  a.out2 = bf.fcur;
+  a.partial = bf.part;
+  a.nchunk = bf.nchunk;
+  return run_forward(f, z, B, bf, OM_RESID, &a, s);
+}
+// the same, synchronously, with the per-sample sums of squares on the host
 int eval_resid(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
                const float* gprev, int B, Bufs& bf, std::vector<double>& host_sumsq, hipStream_t s) {
-  OutArgs a;
-  memset(&a, 0, sizeof(a));
-  a.in0 = xemb;
-  a.in1 = zsub;
-  a.in2 = gprev;
-  a.out0 = gout;
-  a.out1 = dg;
-  a.out2 = bf.fcur;
-  a.partial = bf.part;
-  a.nchunk = bf.nchunk;
-  INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
+  INF_TRY(eval_resid_part(f, z, zsub, xemb, gout, dg, gprev, B, bf, s));
   return read_sumsq(f, B, bf, host_sumsq, s);
-}
-int eval_resid_async(InfNet* f, const float* z, const float* zsub, const float* xemb, float* gout, float* dg,
-                     const float* gprev, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
-  OutArgs a;
-  memset(&a, 0, sizeof(a));
-  a.in0 = xemb;
-  a.in1 = zsub;
-  a.in2 = gprev;
-  a.out0 = gout;
-  a.out1 = dg;
-  a.out2 = bf.fcur;
-  a.partial = bf.part;
-  a.nchunk = bf.nchunk;
-  INF_TRY(run_forward(f, z, B, bf, OM_RESID, &a, s));
-  return enqueue_sumsq(f, B, bf, sl, s);
 }
 
 // vjp residual of the implicit backward (implicit_block.py:186-190): g = (y + y^T J) - grad
-int vjp_resid_async(InfNet* f, const float* y, const float* zi, const float* gradi, float* gout, float* dg,
-                    const float* gprev, int B, Bufs& bf, SumsSlot* sl, hipStream_t s) {
+int vjp_resid_part(InfNet* f, const float* y, const float* zi, const float* gradi, float* gout, float* dg,
+                   const float* gprev, int B, Bufs& bf, hipStream_t s) {
   INF_TRY(run_vjp(f, y, bf.tmp, zi, nullptr, nullptr, B, bf, s));
-  INF_TRY(launch_vjp_resid(bf.tmp, y, gradi, gprev, gout, dg, bf.part, B, f->d, f->fc ? 1 : bf.nchunk, f->fc, s));
-  return enqueue_sumsq(f, B, bf, sl, s);
+  return launch_vjp_resid(bf.tmp, y, gradi, gprev, gout, dg, bf.part, B, f->d, f->fc ? 1 : bf.nchunk, f->fc, s);
 }
 
 double total(const std::vector<double>& v) {
@@ -504,29 +528,73 @@ bool same_shape(const InfNet* a, const InfNet* b) {
 
 // Broyden root find on internal-layout buffers.  Solves z with g(z) = xemb - f(z) - z = 0.
 // Result (lowest iterate) in bf.lowest.  y (internal) is the Banach fallback start.
-// residual g(x) -> gout (+ dg = g - gprev when gprev), per-sample sums of squares -> host
-// (enqueue only: the per-sample sums of squares land in the slot, wait_sumsq retrieves them)
-using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev, SumsSlot* sl)>;
+// resid(x, gout, dg, gprev): residual g(x) -> gout (+ dg = g - gprev when gprev), per-sample partial sums of
+// squares -> bf.part, and (root solves) f(x) -> bf.fcur.  broyden_core reduces and reads them back.
+using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev)>;
+
+// Copies the per-sample results (INF_CONV_PER_SAMPLE) into the stats and the caller's optional host arrays.
+static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vector<double>& lowest_ss,
+                      hipStream_t s) {
+  const int stride = PS_HEAD + T;
+  std::vector<double> st((size_t)B * stride);
+  INF_HIP(hipMemcpyAsync(st.data(), bf.ps_state, sizeof(double) * st.size(), hipMemcpyDeviceToHost, s));
+  INF_HIP(hipStreamSynchronize(s));
+  int nmax = 0, lmax = 0, prot = 0;
+  double d2 = 0.0;
+  lowest_ss.assign(B, 0.0);
+  for (int b = 0; b < B; ++b) {
+    const double* p = st.data() + (size_t)b * stride;
+    const int ns = (int)p[3], ls = (int)p[4], pb = (int)p[5];
+    nmax = std::max(nmax, ns);
+    lmax = std::max(lmax, ls);
+    prot |= pb;
+    lowest_ss[b] = p[1] * p[1];
+    d2 += lowest_ss[b];
+    if (stats.sample_nstep) stats.sample_nstep[b] = ns;
+    if (stats.sample_lowest_step) stats.sample_lowest_step[b] = ls;
+    if (stats.sample_prot_break) stats.sample_prot_break[b] = pb;
+  }
+  stats.nstep = nmax;
+  stats.lowest_step = lmax;
+  stats.prot_break = prot;
+  stats.diff = sqrt(d2);
+  return INF_OK;
+}
 
 // broyden.py:123-193 with the residual as a callback; the result (lowest iterate) is in bf.lowest.
+// f->convergence selects the stopping rule: INF_CONV_GLOBAL is the reference's (one Frobenius norm over the
+// batch against eps sqrt(B d), one lowest iterate for the batch); INF_CONV_PER_SAMPLE runs the same rules per
+// sample against eps sqrt(d) (the reference's result for a batch of one, i.e. independent of how the batch is
+// sharded), with the decisions taken on the device (ps_decide_kernel) and stopped samples frozen.
+// stats.sample_* (host arrays, nullable) receive the per-sample outcome in that mode.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
                  std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
+  const bool per_sample = f->convergence == INF_CONV_PER_SAMPLE;
   std::vector<double> ss(B);
   lowest_ss.assign(B, 0.0);
   const double eps = eps_in * sqrt((double)E);                       // broyden.py:131
-  memset(&stats, 0, sizeof(stats));
-  stats.eps = eps;
+  const double eps_ps = eps_in * sqrt((double)f->d);                 // the same rule for a batch of one
+  {
+    int *a = stats.sample_nstep, *b = stats.sample_lowest_step, *c = stats.sample_prot_break;
+    memset(&stats, 0, sizeof(stats));
+    stats.sample_nstep = a;
+    stats.sample_lowest_step = b;
+    stats.sample_prot_break = c;
+  }
+  stats.eps = per_sample ? eps_ps : eps;
+  stats.convergence = f->convergence;
 
   // One iteration of lookahead: while the host waits for iteration k's residual norm (the reference's
   // .item(), broyden.py:157), iteration k+1's low-rank update and residual are already queued behind it, so
   // the GPU does not idle through the host round trip.  If k stops the loop, k+1's work is discarded: it
-  // only wrote scratch.  Iterates rotate through {xa, xb, lowest} and f(z) through {fcur, flow, fspec}: the
-  // decided lowest, the pending and the speculative one are always distinct buffers; the lowest iterate
-  // (broyden.py:159-162) is tracked by pointer and the Bufs pointers are permuted at the end so that
-  // bf.lowest / bf.flow name the result.
+  // only wrote scratch (per-sample mode: the device decisions of step k already froze every sample it
+  // stopped).  Iterates rotate through {xa, xb, lowest} and f(z) through {fcur, flow, fspec}: the decided
+  // lowest, the pending and the speculative one are always distinct buffers; the lowest iterate
+  // (broyden.py:159-162) is tracked by pointer (per-sample mode: copied per sample into ps_lowx / ps_lowf) and
+  // the Bufs pointers are permuted at the end so that bf.lowest / bf.flow name the result.
   float* xpool[3] = {bf.xa, bf.xb, bf.lowest};
   float* fpool[3] = {bf.fcur, bf.flow, bf.fspec};
   auto pick = [](float* const* pool, const float* a, const float* b) {
@@ -537,27 +605,42 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   SumsSlot* slot[2];
   INF_TRY(sums_slot(0, B, &slot[0]));
   INF_TRY(sums_slot(1, B, &slot[1]));
+  PsStep ps;
+  ps.on = per_sample;
+  ps.T = T;
+  ps.eps = eps_ps;
+  ps.sb = sb;
+  ps.si = si;
+  auto sums = [&](int k, const float* xk, const float* fk, SumsSlot* sl) {
+    ps.k = k;
+    ps.x = xk;
+    ps.f = keep_f ? fk : nullptr;
+    return enqueue_sumsq(f, B, bf, sl, s, &ps);
+  };
   float *gx = bf.ga, *gn = bf.gb;
   float* x = xpool[0];
-  float *low = x, *flow = nullptr;
+  float *low = per_sample ? bf.ps_lowx : x, *flow = nullptr;
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
   INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
   bf.fcur = fpool[0];
-  INF_TRY(resid(x, gx, nullptr, nullptr, slot[0]));
-  if (keep_f) flow = bf.fcur;
+  INF_TRY(resid(x, gx, nullptr, nullptr));
+  INF_TRY(sums(0, x, bf.fcur, slot[0]));
+  if (keep_f) flow = per_sample ? bf.ps_lowf : bf.fcur;
   // iteration 1 is queued before the initial norm is read (update = -g0, x1 = x0 + update, :144)
   float* xp = nullptr;
   float* fp = nullptr;
   if (T > 0) {
-    xp = pick(xpool, low, nullptr);
+    xp = pick(xpool, low, x);
     INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
     INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
-    fp = pick(fpool, flow, nullptr);
+    fp = pick(fpool, flow, bf.fcur);
     bf.fcur = fp;
-    INF_TRY(resid(xp, gn, bf.dg, gx, slot[1]));
+    INF_TRY(resid(xp, gn, bf.dg, gx));
+    INF_TRY(sums(1, xp, fp, slot[1]));
   }
-  INF_TRY(wait_sumsq(slot[0], B, ss));
+  int n_active = B;
+  INF_TRY(wait_sumsq(slot[0], B, ss, &n_active));
   const double init = sqrt(total(ss));
   double obj = init, lowest = init;
   lowest_ss = ss;
@@ -585,61 +668,80 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     ba.part = bf.bpart;
     ba.m = (step - 1) % T;
     ba.ncols = std::min(step, T);
+    ba.active = per_sample ? bf.ps_active : nullptr;
     return launch_broyden_update(ba, s);
   };
-  if (obj >= eps && nstep < T) {                                      // broyden.py:153
-    int ps = 1;
+  const bool go = per_sample ? (n_active > 0 && T > 0) : (obj >= eps && nstep < T);   // broyden.py:153
+  if (go) {
+    int ps_ = 1;
     double prev_obj = -1.0;
     for (;;) {
-      // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps]).  The next
+      // pending = iteration nstep + 1 (iterate xp, residual in gn, f in fp, norms in slot[ps_]).  The next
       // iteration is queued before the pending norm is read, unless the threshold forbids it or the
       // observed contraction predicts that the pending iteration converges (then it would be wasted work).
       const bool allow = nstep + 1 < T;
-      const bool likely_last = prev_obj > 0.0 && obj * (obj / prev_obj) < eps;
+      const bool likely_last = !per_sample && prev_obj > 0.0 && obj * (obj / prev_obj) < eps;
       float *xs = nullptr, *fs = nullptr;
       auto enqueue_next = [&](int pending_step) -> int {
         xs = pick(xpool, low, xp);
         INF_TRY(update(pending_step, xp, gn, xs));
         fs = pick(fpool, flow, fp);
         bf.fcur = fs;
-        return resid(xs, gx, bf.dg, gn, slot[1 - ps]);
+        INF_TRY(resid(xs, gx, bf.dg, gn));
+        return sums(pending_step + 1, xs, fs, slot[1 - ps_]);
       };
       const bool spec = allow && !likely_last;
       if (spec) INF_TRY(enqueue_next(nstep + 1));
-      INF_TRY(wait_sumsq(slot[ps], B, ss));
+      INF_TRY(wait_sumsq(slot[ps_], B, ss, &n_active));
       nstep += 1;
       x = xp;
       prev_obj = obj;
       obj = sqrt(total(ss));
       trace.push_back(obj);
-      if (obj < lowest) {                                               // :159-162
-        low = xp;
-        if (keep_f) flow = fp;
-        lowest = obj;
-        lowest_step = nstep;
-        lowest_ss = ss;
-      }
-      if (obj < eps) break;
-      if (obj < 3 * eps && nstep == T) {                                // :165-168
-        const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
-        double mx = trace[k0], mn = trace[k0];
-        for (size_t k = k0; k < trace.size(); ++k) {
-          mx = std::max(mx, trace[k]);
-          mn = std::min(mn, trace[k]);
+      if (per_sample) {
+        if (n_active == 0 || !allow) break;
+      } else {
+        if (obj < lowest) {                                             // :159-162
+          low = xp;
+          if (keep_f) flow = fp;
+          lowest = obj;
+          lowest_step = nstep;
+          lowest_ss = ss;
         }
-        if (mx / mn < 1.3) break;
+        if (obj < eps) break;
+        if (obj < 3 * eps && nstep == T) {                              // :165-168
+          const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
+          double mx = trace[k0], mn = trace[k0];
+          for (size_t k = k0; k < trace.size(); ++k) {
+            mx = std::max(mx, trace[k]);
+            mn = std::min(mn, trace[k]);
+          }
+          if (mx / mn < 1.3) break;
+        }
+        if (obj > init * 1e6) {                                         // :169-172
+          stats.prot_break = 1;
+          break;
+        }
+        if (!allow) break;                                              // nstep == T
       }
-      if (obj > init * 1e6) {                                           // :169-172
-        stats.prot_break = 1;
-        break;
-      }
-      if (!allow) break;                                                // nstep == T
       if (!spec) INF_TRY(enqueue_next(nstep));
       xp = xs;
       fp = fs;
-      ps = 1 - ps;
+      ps_ = 1 - ps_;
       std::swap(gx, gn);                                                // gn: the new pending residual
     }
+  }
+  stats.n_trace = (int)std::min<size_t>(trace.size(), 64);
+  for (int k = 0; k < stats.n_trace; ++k) stats.trace[k] = trace[k];
+  if (per_sample) {
+    // the pool buffers are scratch; the result is the per-sample lowest iterate
+    bf.lowest = bf.ps_lowx;
+    bf.flow = bf.ps_lowf;
+    bf.xa = xpool[0];
+    bf.xb = xpool[1];
+    bf.fcur = fpool[0];
+    bf.fspec = fpool[2];
+    return ps_collect(bf, B, T, stats, lowest_ss, s);
   }
   // name the result: bf.lowest = the lowest iterate, bf.flow = its f; the other buffers become scratch
   {
@@ -662,8 +764,6 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   stats.nstep = nstep;
   stats.lowest_step = lowest_step;
   stats.diff = lowest;
-  stats.n_trace = (int)std::min<size_t>(trace.size(), 64);
-  for (int k = 0; k < stats.n_trace; ++k) stats.trace[k] = trace[k];
   return INF_OK;
 }
 
@@ -682,39 +782,24 @@ static int ensure_f0(InfNet* f, int B, Bufs& bf, hipStream_t s) {
   return INF_OK;
 }
 
-int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
-                  Bufs& bf, hipStream_t s) {
+// find_fixed_point (implicit_block.py:17-28) of z <- x_embed - f(z) from z0 = y (internal layout):
+//   x, x_prev = g(y), y; while not all((x - x_prev)^2 / (eps + eps |y|) < 1): x, x_prev = g(x), x; i += 1;
+//   break once i > threshold.
+// todo == nullptr: the reference's batch-wide test (torch.all over the batch), result for every sample in
+// bf.lowest.  todo (host, B flags): the same loop per sample (a batch of one each, in lockstep launches); only
+// the flagged samples' rows of bf.lowest are replaced.  *iters = the loop's i.
+static int banach_solve(InfNet* f, const float* y, int B, double eps_in, int threshold, const int* todo, Bufs& bf,
+                        hipStream_t s, int* iters) {
   const size_t E = (size_t)B * f->d;
-  InfBroydenStats stats;
-  std::vector<double> lowest_ss;
-  INF_TRY(ensure_f0(f, B, bf, s));
-  bool first = !f->fc;           // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached
-  const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev, SumsSlot* sl) {
-    if (first) {
-      first = false;
-      INF_TRY(launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s));
-      return enqueue_sumsq(f, B, bf, sl, s);
-    }
-    return eval_resid_async(f, x, x, bf.xemb, gout, dg, gprev, B, bf, sl, s);
-  };
-  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
-  if (diff_detail) {
-    std::vector<float> dd(B);
-    for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
-    INF_HIP(hipMemcpyAsync(diff_detail, dd.data(), sizeof(float) * B, hipMemcpyHostToDevice, s));
-    INF_HIP(hipStreamSynchronize(s));
-  }
-  if (stats.prot_break) {
-    // banach_find_root (implicit_block.py:57-65): z <- x_embed - f(z) from z0 = y, <= 1000 iterations
-    float *zc = bf.xa, *zn = bf.xb;
-    INF_HIP(hipMemsetAsync(bf.zero, 0, sizeof(float) * E, s));
-    INF_HIP(hipMemcpyAsync(zc, y, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
-    std::vector<double> dummy(B);
-    int it = 0;
-    // x = g(y)
-    INF_TRY(eval_resid(f, zc, bf.zero, bf.xemb, zn, nullptr, nullptr, B, bf, dummy, s));
-    std::swap(zc, zn);   // zc = x, zn = x_prev (= y)
-    INF_HIP(hipMemcpyAsync(zn, y, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
+  float *zc = bf.xa, *zn = bf.xb;
+  INF_HIP(hipMemsetAsync(bf.zero, 0, sizeof(float) * E, s));
+  std::vector<double> dummy(B);
+  int it = 0;
+  // x = g(y), x_prev = y
+  INF_TRY(eval_resid(f, y, bf.zero, bf.xemb, zc, nullptr, nullptr, B, bf, dummy, s));
+  INF_HIP(hipMemcpyAsync(zn, y, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+  if (!todo) {
     for (;;) {
       unsigned int bad = 0;
       INF_HIP(hipMemsetAsync(bf.counter, 0, sizeof(unsigned int), s));
@@ -725,9 +810,79 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
       INF_TRY(eval_resid(f, zc, bf.zero, bf.xemb, zn, nullptr, nullptr, B, bf, dummy, s));
       std::swap(zc, zn);
       it += 1;
-      if (it > 1000) break;
+      if (it > threshold) break;
     }
     INF_HIP(hipMemcpyAsync(bf.lowest, zc, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+    *iters = it;
+    return INF_OK;
+  }
+  std::vector<int> flags(todo, todo + B);
+  INF_HIP(hipMemcpyAsync(bf.ps_improved, flags.data(), sizeof(int) * B, hipMemcpyHostToDevice, s));
+  for (;;) {
+    INF_TRY(launch_ps_fixed_point(zc, zn, y, bf.lowest, bf.ps_improved, B, f->d, sb, si, (float)eps_in, 0, s));
+    INF_HIP(hipMemcpyAsync(flags.data(), bf.ps_improved, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+    INF_HIP(hipStreamSynchronize(s));
+    bool any = false;
+    for (int b = 0; b < B; ++b) any = any || flags[b];
+    if (!any) break;
+    INF_TRY(eval_resid(f, zc, bf.zero, bf.xemb, zn, nullptr, nullptr, B, bf, dummy, s));
+    std::swap(zc, zn);
+    it += 1;
+    if (it > threshold) {      // the remaining samples take the latest iterate
+      INF_TRY(launch_ps_fixed_point(zc, zn, y, bf.lowest, bf.ps_improved, B, f->d, sb, si, (float)eps_in, 1, s));
+      break;
+    }
+  }
+  *iters = it;
+  return INF_OK;
+}
+
+// A zeroed stats struct carrying the caller's optional per-sample host arrays.
+static InfBroydenStats stats_for(const InfBroydenStats* caller) {
+  InfBroydenStats st;
+  memset(&st, 0, sizeof(st));
+  if (caller) {
+    st.sample_nstep = caller->sample_nstep;
+    st.sample_lowest_step = caller->sample_lowest_step;
+    st.sample_prot_break = caller->sample_prot_break;
+  }
+  return st;
+}
+
+int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
+                  Bufs& bf, hipStream_t s) {
+  InfBroydenStats stats = stats_for(st);
+  std::vector<double> lowest_ss;
+  INF_TRY(ensure_f0(f, B, bf, s));
+  bool first = !f->fc;           // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached
+  const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev) {
+    if (first) {
+      first = false;
+      return launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s);
+    }
+    return eval_resid_part(f, x, x, bf.xemb, gout, dg, gprev, B, bf, s);
+  };
+  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
+  if (diff_detail) {
+    std::vector<float> dd(B);
+    for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
+    INF_HIP(hipMemcpyAsync(diff_detail, dd.data(), sizeof(float) * B, hipMemcpyHostToDevice, s));
+    INF_HIP(hipStreamSynchronize(s));
+  }
+  if (stats.prot_break) {
+    // banach_find_root (implicit_block.py:57-65,74-75): z <- x_embed - f(z) from z0 = y, <= 1000 iterations;
+    // per-sample mode: only the samples whose own solve broke, each with its own stopping test
+    std::vector<int> todo;
+    if (f->convergence == INF_CONV_PER_SAMPLE) {
+      const int stride = PS_HEAD + T;
+      std::vector<double> pst((size_t)B * stride);
+      INF_HIP(hipMemcpyAsync(pst.data(), bf.ps_state, sizeof(double) * pst.size(), hipMemcpyDeviceToHost, s));
+      INF_HIP(hipStreamSynchronize(s));
+      todo.resize(B);
+      for (int b = 0; b < B; ++b) todo[b] = (int)pst[(size_t)b * stride + 5];
+    }
+    int it = 0;
+    INF_TRY(banach_solve(f, y, B, eps_in, 1000, todo.empty() ? nullptr : todo.data(), bf, s, &it));
     stats.fixed_point_iters = it;
   }
   if (st) *st = stats;
@@ -1055,10 +1210,26 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       // F16X3 planes: 2 fp16 (= 1 float) per element of each of the six operands, plus the scale exponents
       floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64 + 64;
       n->rows_max = std::max(n->rows_max, n->M3);
-      const char* mm = getenv("INFLOW_MFMA");             // "f32" / "bf16x6" / "f16x3" (default)
-      n->mfma_mode = (mm && mm[0] == 'f' && mm[1] == '3') ? INF_MFMA_F32
-                     : (mm && mm[0] == 'b') ? INF_MFMA_BF16X6 : INF_MFMA_F16X3;
+      const char* mm = getenv("INFLOW_MFMA");             // "f32" / "fp32" / "bf16x6" / "f16x3" (default)
+      n->mfma_mode = INF_MFMA_F16X3;
+      if (mm && *mm) {
+        if (!strcmp(mm, "f32") || !strcmp(mm, "fp32")) n->mfma_mode = INF_MFMA_F32;
+        else if (!strcmp(mm, "bf16x6")) n->mfma_mode = INF_MFMA_BF16X6;
+        else if (strcmp(mm, "f16x3") != 0) {
+          fprintf(stderr, "libinflow: INFLOW_MFMA=%s is not one of f32, fp32, bf16x6, f16x3\n", mm);
+          delete n;
+          return INF_ERR_INVALID;
+        }
+      }
     }
+  }
+  {
+    const char* e = getenv("INFLOW_FUSED_K128");            // default of INF_OPT_FUSED_K128
+    if (e && *e) n->k128 = std::min(std::max(atoi(e), 0), 2);
+    e = getenv("INFLOW_EVAL_OVERLAP");                      // default of INF_OPT_EVAL_OVERLAP
+    if (e && *e) n->eval_overlap = e[0] == '1' ? 1 : 0;
+    e = getenv("INFLOW_CONVERGENCE");                       // default of INF_OPT_CONVERGENCE
+    if (e && *e) n->convergence = !strcmp(e, "per_sample") ? INF_CONV_PER_SAMPLE : INF_CONV_GLOBAL;
   }
   // sigma scratch: one partial per 256 output elements of the largest conv (or per channel-split block)
   size_t sc = SIGMA_MAX_PARTS + 64;
@@ -1222,7 +1393,7 @@ int inf_imblock_forward(InfNet* nx, InfNet* nz, const float* x, float* z, int B,
   Bufs bf;
   if (!ws || carve(nx, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
   const float* xi;
-  InfBroydenStats st;
+  InfBroydenStats st = stats_for(stats);
   INF_TRY(root_find_common(nz, nx, x, B, T, eps, &st, nullptr, bf, &xi, s));
   if (stats) *stats = st;
   // z = (nnet_x(x) - nnet_z(z*)) + x   (implicit_block.py:227).  nnet_z(z*) was evaluated by the residual
@@ -1261,10 +1432,10 @@ int inf_imblock_backward(InfNet* nx, InfNet* nz, const float* z, const float* x,
     const float* gi = to_internal(nz, grad, bf.xemb, B, s, &st);
     INF_TRY(st);
     INF_TRY(run_forward(nz, zi, B, bf, -1, nullptr, s));      // activation derivatives at z
-    InfBroydenStats bs;
+    InfBroydenStats bs = stats_for(stats);
     std::vector<double> lowest_ss;
-    const ResidFn resid = [&](const float* y, float* gout, float* dg, const float* gprev, SumsSlot* sl) {
-      return vjp_resid_async(nz, y, zi, gi, gout, dg, gprev, B, bf, sl, s);
+    const ResidFn resid = [&](const float* y, float* gout, float* dg, const float* gprev) {
+      return vjp_resid_part(nz, y, zi, gi, gout, dg, gprev, B, bf, s);
     };
     INF_TRY(broyden_core(nz, resid, B, T, eps, bs, lowest_ss, bf, s));
     if (stats) *stats = bs;
@@ -1401,11 +1572,17 @@ static SideStream* side_stream() {
   return &ss;
 }
 
-// inf_set_eval_overlap: process-wide switch of the overlapped eval schedule below
-static std::atomic<int> g_eval_overlap{[] {
-  const char* e = getenv("INFLOW_EVAL_OVERLAP");
-  return e ? (e[0] == '1' ? 1 : 0) : 1;
-}()};
+// Joins the side stream into the caller's stream when the eval pass returns, on every path after the fork
+// (an error return included): the caller's next call may reuse the workspace the side stream still uses.
+struct SideJoin {
+  SideStream* side = nullptr;
+  hipStream_t s = nullptr;
+  ~SideJoin() {
+    if (!side) return;
+    (void)hipEventRecord(side->join, side->s);
+    (void)hipStreamWaitEvent(s, side->join, 0);
+  }
+};
 
 // Whole eval pass of an imBlock on fused nets (implicit_block.py:220-234 + 245-322 in eval): the x-net's
 // x_embed launch also saves its activation derivatives at x (MODE_EVALSAVE), Broyden solves for z*,
@@ -1429,7 +1606,7 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
   // root solve (sync-bound, and short of work at the 8x8 scale) and then the z-branch series; the two streams join
   // before returning.  Concurrent series launches also desynchronise the CUs' d1/d2 bursts (every 1-WG/CU tile
   // of one launch reads its derivatives in the same phase): 2268 -> 2432 samples/s at B=64 with the 128-pixel VJP.
-  const bool overlap = g_eval_overlap.load(std::memory_order_relaxed) && ws_bytes >= half + zneed + xneed;
+  const bool overlap = nx->eval_overlap && ws_bytes >= half + zneed + xneed;
   if (overlap) {
     carve(nx, B, 1, w0 + half + zneed, xneed, bfc);
     bfc.D = bfa.D;                              // the x_embed pass saves f_x's derivatives into bfa.D
@@ -1454,20 +1631,21 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
     a.out1 = bfa.xemb;
     INF_TRY(launch_conv_out(a, B, s));
   }
-  SideStream* side = nullptr;
+  SideJoin join;
   if (overlap) {
-    side = side_stream();
+    SideStream* side = side_stream();
     if (!side) return INF_ERR_HIP;
     INF_HIP(hipEventRecord(side->fork, s));
     INF_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+    join.side = side;
+    join.s = s;
     InfNet* nets1[1] = {nx};
     const float* xs1[1] = {x};
     const float* es1[1] = {eps_x};
     float* outs1[1] = {logdet_x};
     INF_TRY(series_fused(nets1, xs1, es1, 1, coeff, n_terms, outs1, B, &bfc, side->s, /*save_mask=*/0u));
-    INF_HIP(hipEventRecord(side->join, side->s));
   }
-  InfBroydenStats st;
+  InfBroydenStats st = stats_for(stats);
   INF_TRY(broyden_solve(nz, x, B, T, eps, &st, nullptr, bfa, s));
   if (stats) *stats = st;
   if (!st.prot_break) {
@@ -1485,9 +1663,7 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
     const float* xs1[1] = {z};
     const float* es1[1] = {eps_z};
     float* outs1[1] = {logdet_z};
-    INF_TRY(series_fused(nets1, xs1, es1, 1, coeff, n_terms, outs1, B, &bfb, s, /*save_mask=*/1u));
-    INF_HIP(hipStreamWaitEvent(s, side->join, 0));
-    return INF_OK;
+    return series_fused(nets1, xs1, es1, 1, coeff, n_terms, outs1, B, &bfb, s, /*save_mask=*/1u);   // join: ~SideJoin
   }
   InfNet* nets[2] = {nx, nz};
   const float* xs[2] = {x, z};
@@ -1926,14 +2102,54 @@ size_t inf_grad_workspace_bytes(InfNet* n, int B) {
 
 int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
 
-int inf_set_eval_overlap(int on) {
-  if (on != 0 && on != 1) return -INF_ERR_INVALID;
-  return g_eval_overlap.exchange(on);
+int inf_net_set_option(InfNet* n, int option, int value) {
+  if (!n) return -INF_ERR_INVALID;
+  int* slot = nullptr;
+  int lo = 0, hi = 0;
+  switch (option) {
+    case INF_OPT_FUSED_K128: slot = &n->k128; hi = 2; break;
+    case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
+    case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
+    default: return -INF_ERR_INVALID;
+  }
+  if (value < lo || value > hi) return -INF_ERR_INVALID;
+  const int prev = *slot;
+  *slot = value;
+  return prev;
 }
 
-int inf_set_fused_k128(int policy) {
-  const int prev = inf::set_fused_k128(policy);
-  return prev < 0 ? -INF_ERR_INVALID : prev;
+int inf_net_get_option(const InfNet* n, int option) {
+  if (!n) return -INF_ERR_INVALID;
+  switch (option) {
+    case INF_OPT_FUSED_K128: return n->k128;
+    case INF_OPT_EVAL_OVERLAP: return n->eval_overlap;
+    case INF_OPT_CONVERGENCE: return n->convergence;
+    default: return -INF_ERR_INVALID;
+  }
+}
+
+int inf_banach_find_root(InfNet* f, InfNet* e, const float* y, float* out, int B, int threshold, double eps,
+                         int* iters, void* ws, size_t ws_bytes, void* stream) {
+  if (!f || !e || !y || !out || B <= 0 || threshold < 0 || !same_shape(f, e)) return INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(f, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* yi = to_internal(f, y, bf.xin, B, s, &st);
+  INF_TRY(st);
+  // x_embed = e(y) + y  (implicit_block.py:60)
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = yi;
+  a.out0 = bf.fx;
+  a.out1 = bf.xemb;
+  INF_TRY(run_forward(e, yi, B, bf, OM_EMBED, &a, s));
+  std::vector<int> todo;
+  if (f->convergence == INF_CONV_PER_SAMPLE) todo.assign(B, 1);
+  int it = 0;
+  INF_TRY(banach_solve(f, yi, B, eps, threshold, todo.empty() ? nullptr : todo.data(), bf, s, &it));
+  if (iters) *iters = it;
+  return to_boundary(f, bf.lowest, out, B, s);
 }
 
 }  // extern "C"

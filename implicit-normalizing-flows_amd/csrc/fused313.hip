@@ -595,16 +595,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         float x[8];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) x[kk] = tb[kk * F_BN + 32 * b];
-#ifdef INFLOW_EXP_NOSPLIT      // diagnostic build only (wrong results): no B-operand split VALU
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          o.h[b][j] = __builtin_amdgcn_perm(__float_as_uint(x[2 * j + 1]), __float_as_uint(x[2 * j]), 0x07060302u);
-          o.m[b][j] = 0u;
-          o.l[b][j] = 0u;
-        }
-#else
         split3(x, o.h[b], o.m[b], o.l[b]);
-#endif
       }
     };
     auto bmma = [&](const u32x4 (&af)[TM][3], const BOp& o) {
@@ -632,9 +623,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int kn = kt + d + D - 1;
-#ifdef INFLOW_EXP_NOWLOAD       // diagnostic build only (wrong results): no weight loads after the prologue
-        if (kn < D)
-#elif PB_SCHED
+#if PB_SCHED
         if (true)      // (the last D-1 steps reload the last K tile: one straight-line block per step)
 #else
         if (kn < nkt)
@@ -1120,17 +1109,6 @@ static void timing_collect(const char* key, long nwg, hipStream_t s) {
   }
 }
 
-// VJP / EVAL variant policy (inf_set_fused_k128): 0 the 64-pixel kernel only, 1 the 128-pixel K-chunked kernel where
-// its grid still covers every CU (default; INFLOW_FUSED_K128 in the environment), 2 wherever it fits (tests)
-static std::atomic<int> g_k128{[] {
-  const char* e = getenv("INFLOW_FUSED_K128");
-  return e ? atoi(e) : 1;
-}()};
-int set_fused_k128(int policy) {
-  if (policy < 0 || policy > 2) return -1;
-  return g_k128.exchange(policy);
-}
-
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets) {
   if (layout_nets <= 0) layout_nets = nnets;
   const Net313Args& a0 = args[0];
@@ -1162,7 +1140,9 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool h3_args = pr.a[0].A1h != nullptr && pr.a[1].A1h != nullptr && pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr;
   // 128-pixel K-chunked VJP (fused313k.hip): h3 (all phases), where the pair's derivatives are in the 64-pixel
   // layout and the grid still covers every CU
-  const int k128_pol = g_k128.load(std::memory_order_relaxed);
+  // VJP / EVAL variant policy (per net, INF_OPT_FUSED_K128): 0 the 64-pixel kernel only, 1 the 128-pixel
+  // K-chunked kernel where its grid still covers every CU (default), 2 wherever it fits (tests)
+  const int k128_pol = a0.k128;
   const bool k128 = k128_pol && H3_AC && h3_args && (mode == MODE_VJP || mode == MODE_EVAL) && var == V64 && force_bn == 0 &&
                     force_var < 0 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
                     (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);

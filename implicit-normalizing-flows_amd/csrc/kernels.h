@@ -91,8 +91,19 @@ struct BroydenArgs {
   double* part;   // scratch partials
   int m;          // existing columns (nstep - 1) % T
   int ncols;      // columns used by the update (min(nstep, T))
+  const int* active;   // per-sample mode (nullable): stopped samples keep x (xnew = x) and their U / VT columns
 };
 int launch_broyden_update(const BroydenArgs& a, hipStream_t s);
+
+// per-sample convergence (INF_CONV_PER_SAMPLE, pointwise.hip): the stopping rules of broyden.py:153-172 per sample
+constexpr int PS_HEAD = 8;   // doubles of per-sample state before the objective ring
+// ss: B per-sample sums of squares (+1: receives the number of samples still iterating); k = step (0: initial)
+int launch_ps_decide(double* ss, double* state, int* active, int* improved, int B, int k, int T, double eps,
+                     hipStream_t s);
+int launch_ps_copy(const int* improved, const float* x, const float* f, float* lowx, float* lowf, int B, int d, long sb,
+                   long si, hipStream_t s);
+int launch_ps_fixed_point(const float* x, const float* xp, const float* y, float* result, int* todo, int B, int d,
+                          long sb, long si, float eps, int force, hipStream_t s);
 
 // Spectral scale: sigma = u . (W v) for conv (pad k//2) or matrix; factor = max(1, sigma / coeff)
 constexpr int SIGMA_MAX_PARTS = 4096;   // launch_sigma's partial count bound when it splits channels
@@ -167,6 +178,8 @@ struct Net313Args {
   int dot_nchunk;
   float* acc_w;           // with in_taps: acc_w[img, own pixels] += acc_coef * v (Neumann vector accumulation,
   float acc_coef;         //   implicit_block.py:430-436), v the previous term's VJP after the tap sum
+  int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
+                          //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
 };
 struct Net313Pair {
   Net313Args a[2];
@@ -180,7 +193,6 @@ int net313_supported(int hid, int C, int H, int W);
 // 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
 int net313k_fits(int hid, int C, int H, int W);
 int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s);
-int set_fused_k128(int policy);   // returns the previous policy, -1 for an invalid one
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 // layout_nets (> 0) picks the tile variant as if that many nets shared the grid: launches that write
 // derivatives for a paired series must use the pair's variant (the d1/d2 layout depends on it)

@@ -293,6 +293,15 @@ constexpr int BR_TMAX = 64;
 __global__ __launch_bounds__(256) void broyden_small_kernel(BroydenArgs a) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.batch) return;
+  if (a.active && !a.active[b]) {       // per-sample mode: a stopped sample keeps its iterate and its U / VT
+    for (int i = 0; i < a.d; ++i) {
+      const long e = BR_IDX(b, i);
+      a.xnew[e] = a.x[e];
+      a.dxnew[e] = 0.f;
+      a.upd[e] = 0.f;
+    }
+    return;
+  }
   float aj[BR_TMAX], cj[BR_TMAX];
   for (int j = 0; j < a.m; ++j) {
     const float* U = a.U + (long)j * a.cs;
@@ -355,6 +364,7 @@ __global__ __launch_bounds__(256) void broyden_small_kernel(BroydenArgs a) {
 __global__ __launch_bounds__(256) void broyden_p1(BroydenArgs a, int nchunk) {
   __shared__ double red[16];
   const int b = blockIdx.y, ch = blockIdx.x;
+  if (a.active && !a.active[b]) return;
   const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
   double* out = a.part + ((long)b * nchunk + ch) * 2 * a.T;
   for (int j = 0; j < a.m; ++j) {
@@ -379,6 +389,7 @@ __global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, dou
   __shared__ double red[16];
   __shared__ float coef[2 * BR_TMAX];
   const int b = blockIdx.y, ch = blockIdx.x;
+  if (a.active && !a.active[b]) return;
   for (int j = threadIdx.x; j < 2 * a.m; j += blockDim.x) {
     const int jj = j < a.m ? j : a.T + (j - a.m);
     double s = 0.0;
@@ -409,6 +420,7 @@ __global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, con
   __shared__ double red[16];
   __shared__ float denf;
   const int b = blockIdx.y, ch = blockIdx.x;
+  if (a.active && !a.active[b]) return;
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int c = 0; c < nchunk; ++c) s += part2[(long)b * nchunk + c];
@@ -444,6 +456,16 @@ __global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, con
 __global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, const double* part3) {
   __shared__ float ej[BR_TMAX];
   const int b = blockIdx.y, ch = blockIdx.x;
+  if (a.active && !a.active[b]) {
+    const int lo = ch * BR_CH, hi = min(a.d, lo + BR_CH);
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const long e = BR_IDX(b, i);
+      a.xnew[e] = a.x[e];
+      a.dxnew[e] = 0.f;
+      a.upd[e] = 0.f;
+    }
+    return;
+  }
   for (int j = threadIdx.x; j < a.ncols; j += blockDim.x) {
     double s = 0.0;
     for (int c = 0; c < nchunk; ++c) s += part3[((long)b * nchunk + c) * a.T + j];
@@ -484,6 +506,124 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, part2, part3);
   INF_CHECK_LAUNCH();
   hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, part3);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-sample convergence (INF_CONV_PER_SAMPLE): every sample runs the reference's stopping rules
+// (broyden.py:153-172) on its own residual norm against eps * sqrt(d), i.e. exactly what broyden() returns
+// for a batch of one.  All samples advance in lockstep launches; the state machine lives on the device, so a
+// speculatively queued iteration (engine.hip broyden_core) already sees the decisions of the one before it.
+// state[b * (PS_HEAD + T) + ...]: 0 init, 1 lowest, 2 -, 3 nstep, 4 lowest_step, 5 prot_break, 6 latest,
+// PS_HEAD.. the ring of the last T objectives (step k at (k - 1) % T).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void ps_decide_kernel(double* ss, double* state, int* active, int* improved,
+                                                         int B, int k, int T, double eps) {
+  __shared__ double red[16];
+  double cnt = 0.0;
+  const int stride = PS_HEAD + T;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    double* st = state + (long)b * stride;
+    const double obj = sqrt(ss[b]);
+    int act = 0, imp = 0;
+    if (k == 0) {                                          // broyden.py:145-153
+      st[0] = obj;
+      st[1] = obj;
+      st[3] = 0.0;
+      st[4] = 0.0;
+      st[5] = 0.0;
+      st[6] = obj;
+      act = (obj >= eps && T > 0) ? 1 : 0;
+      imp = 1;                                             // lowest_xest = x0
+    } else if (active[b]) {
+      st[3] = k;
+      st[6] = obj;
+      st[PS_HEAD + (k - 1) % T] = obj;
+      if (obj < st[1]) {                                   // :159-162
+        st[1] = obj;
+        st[4] = k;
+        imp = 1;
+      }
+      act = 1;
+      if (obj < eps) {                                     // :163
+        act = 0;
+      } else {
+        if (obj < 3 * eps && k == T) {                     // :165-168 (trace[-T:] = steps 1..T)
+          double mx = st[PS_HEAD], mn = st[PS_HEAD];
+          for (int j = 1; j < T; ++j) {
+            mx = fmax(mx, st[PS_HEAD + j]);
+            mn = fmin(mn, st[PS_HEAD + j]);
+          }
+          if (mx / mn < 1.3) act = 0;
+        }
+        if (act && obj > st[0] * 1e6) {                    // :169-172
+          st[5] = 1.0;
+          act = 0;
+        }
+        if (k >= T) act = 0;                               // :153
+      }
+    }
+    active[b] = act;
+    improved[b] = imp;
+    cnt += act;
+  }
+  cnt = block_sum(cnt, red);
+  if (threadIdx.x == 0) ss[B] = cnt;
+}
+int launch_ps_decide(double* ss, double* state, int* active, int* improved, int B, int k, int T, double eps,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(ps_decide_kernel, dim3(1), dim3(1024), 0, s, ss, state, active, improved, B, k, T, eps);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+// lowest iterate (and its f) of the improved samples: grid (chunks, B)
+__global__ __launch_bounds__(256) void ps_copy_kernel(const int* improved, const float* x, const float* f,
+                                                      float* lowx, float* lowf, int d, long sb, long si) {
+  const int b = blockIdx.y;
+  if (!improved[b]) return;
+  for (int i = blockIdx.x * 1024 + threadIdx.x; i < min(d, (int)(blockIdx.x + 1) * 1024); i += blockDim.x) {
+    const long e = (long)b * sb + (long)i * si;
+    lowx[e] = x[e];
+    if (f) lowf[e] = f[e];
+  }
+}
+int launch_ps_copy(const int* improved, const float* x, const float* f, float* lowx, float* lowf, int B, int d, long sb,
+                   long si, hipStream_t s) {
+  hipLaunchKernelGGL(ps_copy_kernel, dim3((d + 1023) / 1024, B), dim3(256), 0, s, improved, x, f, lowx, lowf, d, sb,
+                     si);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+// Banach fallback per sample (find_fixed_point, implicit_block.py:17-28, on a batch of one): for every sample
+// still iterating (todo[b]), test sum_i [(x - xp)^2 / (eps + eps |y|) >= 1] == 0; a sample that passes (or every
+// remaining one when `force`) takes x as its result and stops.  One workgroup per sample.
+__global__ __launch_bounds__(256) void ps_fixed_point_kernel(const float* x, const float* xp, const float* y,
+                                                             float* result, int* todo, int d, long sb, long si,
+                                                             float eps, int force) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  if (!todo[b]) return;
+  double bad = 0.0;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    const long e = (long)b * sb + (long)i * si;
+    const float dd = x[e] - xp[e];
+    const float tol = eps + eps * fabsf(y[e]);
+    bad += !((dd * dd) / tol < 1.f) ? 1.0 : 0.0;
+  }
+  bad = block_sum(bad, red);
+  if (bad == 0.0 || force) {
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+      const long e = (long)b * sb + (long)i * si;
+      result[e] = x[e];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) todo[b] = 0;
+  }
+}
+int launch_ps_fixed_point(const float* x, const float* xp, const float* y, float* result, int* todo, int B, int d,
+                          long sb, long si, float eps, int force, hipStream_t s) {
+  hipLaunchKernelGGL(ps_fixed_point_kernel, dim3(B), dim3(256), 0, s, x, xp, y, result, todo, d, sb, si, eps, force);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

@@ -18,6 +18,9 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
+INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE = 1, 2, 3     # InfNetOption
+INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
+CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 
 
 class PowerIterDesc(ctypes.Structure):
@@ -45,13 +48,26 @@ class NetDesc(ctypes.Structure):
 class BroydenStats(ctypes.Structure):
     _fields_ = [('nstep', ctypes.c_int), ('lowest_step', ctypes.c_int), ('prot_break', ctypes.c_int),
                 ('n_trace', ctypes.c_int), ('trace', ctypes.c_double * 64), ('diff', ctypes.c_double),
-                ('eps', ctypes.c_double), ('fixed_point_iters', ctypes.c_int)]
+                ('eps', ctypes.c_double), ('fixed_point_iters', ctypes.c_int), ('convergence', ctypes.c_int),
+                ('sample_nstep', ctypes.POINTER(ctypes.c_int)), ('sample_lowest_step', ctypes.POINTER(ctypes.c_int)),
+                ('sample_prot_break', ctypes.POINTER(ctypes.c_int))]
+
+    def want_samples(self, batch):
+        """Per-sample outcome arrays (INF_CONV_PER_SAMPLE): host buffers the engine fills."""
+        self._samples = [(ctypes.c_int * batch)() for _ in range(3)]
+        self.sample_nstep, self.sample_lowest_step, self.sample_prot_break = [
+            ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in self._samples]
+        return self
 
     def as_dict(self, threshold):
-        return {'nstep': self.nstep, 'tnstep': self.nstep, 'lowest_step': self.lowest_step,
-                'diff': self.diff, 'prot_break': bool(self.prot_break),
-                'trace': [self.trace[i] for i in range(self.n_trace)], 'eps': self.eps,
-                'threshold': threshold, 'fixed_point_iters': self.fixed_point_iters}
+        d = {'nstep': self.nstep, 'tnstep': self.nstep, 'lowest_step': self.lowest_step,
+             'diff': self.diff, 'prot_break': bool(self.prot_break),
+             'trace': [self.trace[i] for i in range(self.n_trace)], 'eps': self.eps,
+             'threshold': threshold, 'fixed_point_iters': self.fixed_point_iters,
+             'convergence': 'per_sample' if self.convergence == INF_CONV_PER_SAMPLE else 'global'}
+        if self.convergence == INF_CONV_PER_SAMPLE and getattr(self, '_samples', None):
+            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in self._samples]
+        return d
 
 
 class KernelStat(ctypes.Structure):
@@ -112,8 +128,10 @@ _SIGS = {
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
-    'inf_set_fused_k128': (ctypes.c_int, [ctypes.c_int]),
-    'inf_set_eval_overlap': (ctypes.c_int, [ctypes.c_int]),
+    'inf_net_set_option': (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
+    'inf_net_get_option': (ctypes.c_int, [_P, ctypes.c_int]),
+    'inf_banach_find_root': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                            ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),
     'inf_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int]),
     'inf_net_param_grad': (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t,
                                           _P]),
@@ -238,6 +256,16 @@ class NativeNet:
         if st != self._stamp:
             check(self.lib.inf_net_refresh(self.handle, stream), 'inf_net_refresh')
             self._stamp = st
+
+    def set_option(self, option, value):
+        """inf_net_set_option; returns the previous value."""
+        prev = self.lib.inf_net_set_option(self.handle, int(option), int(value))
+        if prev < 0:
+            raise HipError('inf_net_set_option(%d, %d): invalid option or value' % (option, value))
+        return prev
+
+    def get_option(self, option):
+        return self.lib.inf_net_get_option(self.handle, int(option))
 
     def ws_bytes(self, batch, threshold=1):
         return int(self.lib.inf_workspace_bytes(self.handle, int(batch), int(threshold)))

@@ -39,3 +39,23 @@ def build_flow(arch, batch=64):
 
 def imblocks(model):
     return [m for m in model.modules() if isinstance(m, layers.imBlock)]
+
+
+def engine_nets(model):
+    """The engine nets (lib._hip.NativeNet) the model's imBlocks have created so far (after a first forward)."""
+    out = []
+    for blk in imblocks(model):
+        for net in (blk.nnet_x, blk.nnet_z):
+            out.extend(net.__dict__.get('_inf_native', {}).values())
+    return out
+
+
+def set_engine_option(model, option, value):
+    """inf_net_set_option on every engine net of the model; returns {net: previous value} for restore_engine_options.
+    The options are per net (no process-wide switch), so this touches only this model's nets."""
+    return {n: n.set_option(option, value) for n in engine_nets(model)}
+
+
+def restore_engine_options(option, previous):
+    for n, v in previous.items():
+        n.set_option(option, v)

@@ -33,10 +33,10 @@ import torch.nn as nn
 from .. import _hip
 from . import netgrad, solvers
 
-__all__ = ['imBlock', 'set_probe_mode']
+__all__ = ['imBlock', 'set_probe_mode', 'set_probe_shard', 'set_convergence', 'RootFind']
 
-_PROBES = {'mode': 'reference', 'seed': 0, 'offset': 0}
-
+_PROBES = {'mode': 'reference', 'seed': 0, 'offset': 0, 'shard': None}
+_SOLVE = {'convergence': 'global'}
 
 
 def set_probe_mode(mode, seed=0):
@@ -46,10 +46,53 @@ def set_probe_mode(mode, seed=0):
     _PROBES.update(mode=mode, seed=int(seed), offset=0)
 
 
+def set_probe_shard(lo=None, hi=None, global_batch=None):
+    """Sharded evaluation (one process per GPU, rows [lo, hi) of a global batch): every probe tensor is drawn for
+    the GLOBAL batch in the reference's order and the shard keeps its rows, so each rank sees exactly the probes
+    the single-process run gives those samples ('reference' mode: the torch CPU stream; 'device' mode: the same
+    counter-based stream offset by the shard's first element).  set_probe_shard() turns it off."""
+    if lo is None:
+        _PROBES['shard'] = None
+        return
+    if not (0 <= lo <= hi <= global_batch):
+        raise ValueError((lo, hi, global_batch))
+    _PROBES['shard'] = (int(lo), int(hi), int(global_batch))
+
+
+def set_convergence(mode):
+    """Default Broyden stopping rule of imBlock root solves: 'global' (the reference's: one norm over the batch,
+    broyden.py:131,153-163) or 'per_sample' (each sample stops on its own norm: the reference's result for a batch
+    of one, invariant to sharding).  An imBlock's ``convergence`` attribute overrides it."""
+    if mode not in _hip.CONVERGENCE:
+        raise ValueError(mode)
+    _SOLVE['convergence'] = mode
+
+
 def _probes(shape, device):
-    out = solvers.rademacher_probes(shape, device, _PROBES['mode'], _PROBES['seed'], _PROBES['offset'])
-    _PROBES['offset'] += int(np.prod(shape))
+    shard = _PROBES['shard']
+    per = int(np.prod(shape[1:]))
+    if shard is None or shard[2] == shape[0] and shard[0] == 0:
+        out = solvers.rademacher_probes(shape, device, _PROBES['mode'], _PROBES['seed'], _PROBES['offset'])
+        _PROBES['offset'] += int(np.prod(shape))
+        return out
+    lo, hi, n = shard
+    if hi - lo != shape[0]:
+        raise ValueError('probe shard [%d, %d) of %d does not match a batch of %d' % (lo, hi, n, shape[0]))
+    if _PROBES['mode'] == 'reference':       # the global draw, this shard's rows
+        out = solvers.rademacher_probes((n,) + tuple(shape[1:]), 'cpu', 'reference')[lo:hi].contiguous()
+        out = out.to(device, non_blocking=True)
+    else:
+        out = solvers.rademacher_probes(shape, device, 'device', _PROBES['seed'], _PROBES['offset'] + lo * per)
+    _PROBES['offset'] += n * per
     return out
+
+
+def _stats(B, nets):
+    """BroydenStats for a solve on `nets` (per-sample outcome arrays in per-sample mode)."""
+    st = _hip.BroydenStats()
+    if any(n.get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE for n in nets):
+        st.want_samples(B)
+    return st
 
 
 class _ImplicitBackward(torch.autograd.Function):
@@ -72,7 +115,7 @@ class _ImplicitBackward(torch.autograd.Function):
         ws = _hip.workspace(x.device, max(nz.ws_bytes(B, T), nx.ws_bytes(B, 1)))
         grad = grad.contiguous()
         dl_dh, dl_dx = torch.empty_like(grad), torch.empty_like(grad)
-        st = _hip.BroydenStats()
+        st = _stats(B, (nz,))
         _hip.check(_hip.load().inf_imblock_backward(nx.handle, nz.handle, _hip.ptr(z.contiguous()),
                                                     _hip.ptr(x.contiguous()), _hip.ptr(grad), _hip.ptr(dl_dh),
                                                     _hip.ptr(dl_dx), B, T, float(blk.eps_backward), ctypes.byref(st),
@@ -163,6 +206,48 @@ class _MemEffNeumannNative(torch.autograd.Function):
         return (gx * dL, None, None, None, None) + tuple(g * dL if g is not None else None for g in ctx.grads)
 
 
+class RootFind:
+    """RootFind.apply(nnet_z, nnet_x, z0, x, method, eps, threshold) (implicit_block.py:51-100): the root z of
+    z + nnet_z(z) = x + nnet_x(x), by 'broyden' (from 0, Banach fallback on prot_break; inf_root_find) or 'banach'
+    (find_fixed_point from z0, :57-65; inf_banach_find_root).  No gradient (the reference's backward asserts).
+    The solve's statistics are left in RootFind.last (dict)."""
+    last = None
+
+    @staticmethod
+    def apply(nnet_z, nnet_x, z0, x, method, *args):
+        eps, threshold = float(args[-2]), int(args[-1])
+        _hip.require_device(x, 'RootFind')
+        if method not in ('broyden', 'banach'):
+            raise ValueError(method)
+        if z0 is not x and not torch.equal(z0, x):
+            raise NotImplementedError('z0 must equal x (the only use in the reference, implicit_block.py:226,238)')
+        lib = _hip.load()
+        x = x.contiguous()
+        B = x.shape[0]
+        stream = _hip.stream_of(x)
+        nets = []
+        for net in (nnet_z, nnet_x):
+            n = _hip.native_net(net, x.shape[1:], x.device)
+            n.refresh_if_needed(stream)
+            nets.append(n)
+        nf, ne = nets
+        out = torch.empty_like(x)
+        if method == 'broyden':
+            ws = _hip.workspace(x.device, max(nf.ws_bytes(B, threshold), ne.ws_bytes(B, threshold)))
+            st = _stats(B, (nf,))
+            _hip.check(lib.inf_root_find(nf.handle, ne.handle, _hip.ptr(x), _hip.ptr(out), B, threshold, eps,
+                                         ctypes.byref(st), None, _hip.ptr(ws), ws.numel(), stream), 'inf_root_find')
+            RootFind.last = st.as_dict(threshold)
+        else:
+            ws = _hip.workspace(x.device, max(nf.ws_bytes(B), ne.ws_bytes(B)))
+            it = ctypes.c_int()
+            _hip.check(lib.inf_banach_find_root(nf.handle, ne.handle, _hip.ptr(x), _hip.ptr(out), B, threshold, eps,
+                                                ctypes.byref(it), _hip.ptr(ws), ws.numel(), stream),
+                       'inf_banach_find_root')
+            RootFind.last = {'fixed_point_iters': it.value}
+        return out
+
+
 def _needs_graph(module, *ts):
     return torch.is_grad_enabled() and (any(t.requires_grad for t in ts) or
                                         any(p.requires_grad for p in module.parameters()))
@@ -206,6 +291,7 @@ class imBlock(nn.Module):
         self.register_buffer('last_firmom', torch.zeros(1))
         self.register_buffer('last_secmom', torch.zeros(1))
         self.last_broyden = None
+        self.convergence = None          # None: the module default (set_convergence); 'global' / 'per_sample'
 
     # ---------------------------------------------------------------------------------------
     def _native(self, t):
@@ -218,10 +304,13 @@ class imBlock(nn.Module):
                         net(t[:1])
             self.__dict__['_convs_ready'] = True
         stream = _hip.stream_of(t)
+        conv = _hip.CONVERGENCE[getattr(self, 'convergence', None) or _SOLVE['convergence']]
         nets = []
         for net in (self.nnet_x, self.nnet_z):
             n = _hip.native_net(net, shape, t.device)
             n.refresh_if_needed(stream)
+            if n.get_option(_hip.INF_OPT_CONVERGENCE) != conv:
+                n.set_option(_hip.INF_OPT_CONVERGENCE, conv)
             nets.append(n)
         return nets[0], nets[1], stream
 
@@ -372,7 +461,7 @@ class imBlock(nn.Module):
         T = int(self.threshold)
         ws = _hip.workspace(y.device, max(net_f.ws_bytes(B, T), net_e.ws_bytes(B, T)))
         out = torch.empty_like(y)
-        st = _hip.BroydenStats()
+        st = _stats(B, (net_f,))
         if forward:
             rc = lib.inf_imblock_forward(net_e.handle, net_f.handle, _hip.ptr(y), _hip.ptr(out), B, T, float(eps),
                                          ctypes.byref(st), _hip.ptr(ws), ws.numel(), stream)
@@ -420,7 +509,7 @@ class imBlock(nn.Module):
         ws = _hip.workspace(x.device, nx.ws_bytes(B, T) + nz.ws_bytes(B, 1) + nx.ws_bytes(B, 1))
         z = torch.empty_like(x)
         out = torch.empty(2, B, device=x.device)
-        st = _hip.BroydenStats()
+        st = _stats(B, (nz,))
         rc = lib.inf_imblock_eval(nx.handle, nz.handle, _hip.ptr(x), _hip.ptr(z), _hip.ptr(probes[0]),
                                   _hip.ptr(probes[1]), co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps,
                                   _hip.ptr(out[0]), _hip.ptr(out[1]), B, T, float(self.eps_forward), ctypes.byref(st),

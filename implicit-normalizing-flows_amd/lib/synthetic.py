@@ -269,3 +269,33 @@ def checkerboard_batch(B, seed=0):
     x2_ = rs.rand(B) - rs.randint(0, 2, B) * 2
     x2 = x2_ + (np.floor(x1) % 2)
     return torch.from_numpy(np.concatenate([x1[:, None], x2[:, None]], 1) * 2).float()
+
+
+# Layers of the power-iteration fixtures (tests/golden/make_golden_edges.py power_iter_layers):
+POWER_ITER_LAYERS = [   # (arch, key, kind, cin, cout, k, hw, n_iterations, perturbation scale)
+    ('cifar10', 'transforms.0.chain.2.nnet_x.0', 'conv', 3, 512, 3, (32, 32), None, 0.5),
+    ('cifar10', 'transforms.0.chain.2.nnet_x.2', 'conv', 512, 512, 1, (32, 32), None, 0.5),
+    ('cifar10', 'transforms.0.chain.2.nnet_x.4', 'conv', 512, 3, 3, (32, 32), None, 0.5),
+    ('cifar10', 'transforms.1.chain.0.nnet_z.1', 'conv', 12, 512, 3, (16, 16), None, 1.0),
+    ('cifar10', 'transforms.2.chain.2.nnet_z.5', 'conv', 512, 48, 3, (8, 8), None, 1.0),
+    ('cifar10', 'transforms.2.chain.0.nnet_x.3', 'conv', 512, 512, 1, (8, 8), 7, 0.05),
+    ('cifar10', 'transforms.0.chain.4.nnet_z.1', 'conv', 3, 512, 3, (32, 32), None, 0.05),
+    ('power', 'chain.0.nnet_x.0', 'linear', 6, 128, 1, None, None, 0.05),
+    ('power', 'chain.3.nnet_z.2', 'linear', 128, 128, 1, None, None, 0.5),
+]
+
+
+def perturbed_weight(sd, key, seed=1, scale=0.05):
+    """sd[key + '.weight'] moved off its converged u / v (as after an optimiser step): W + scale * std(W) * N(0, 1),
+    deterministic (numpy PCG64 keyed like the weights).  Power-iteration fixtures start from it."""
+    W = sd[key + '.weight'].numpy().astype(np.float32)
+    noise = _rng(seed + 1000, key).standard_normal(W.shape).astype(np.float32)
+    return torch.from_numpy(W + np.float32(scale * float(W.std())) * noise)
+
+
+def vec_summary(v, key):
+    """Size-independent summary of a long vector for fixtures: sum, sum of squares, a seeded +-1 projection
+    (numpy PCG64 keyed by `key`), and the first 64 entries."""
+    v = np.asarray(v, dtype=np.float64).ravel()
+    sign = _rng(7, key).integers(0, 2, v.size).astype(np.float64) * 2 - 1
+    return np.array([v.sum(), (v * v).sum(), (v * sign).sum()]), v[:64].astype(np.float32)

@@ -12,7 +12,11 @@
  *     iteration back to the host exactly where the reference calls .item() (broyden.py:145,157);
  *   - workspace is caller-allocated (inf_workspace_bytes) so the torch caching allocator owns it;
  *   - return value 0 = success, otherwise an InfStatus code (inf_status_string()).
- *   - no global mutable state: calls are re-entrant across streams/threads for distinct workspaces.
+ *   - no process-wide mutable state: every tuning / semantics switch is a per-net option
+ *     (inf_net_set_option), the launch profiler is per host thread, and the host readback buffers and the
+ *     side stream of inf_imblock_eval are per host thread.  Calls are re-entrant across threads for
+ *     distinct nets and workspaces.  A net handle itself (its packed weights, its option values and its cached
+ *     f(0) for the first Broyden residual) belongs to one thread at a time, like the nn.Module it mirrors.
  */
 #ifndef INFLOW_H
 #define INFLOW_H
@@ -59,14 +63,20 @@ typedef struct InfNetDesc {
 typedef struct InfNet InfNet;   /* opaque: packed, Lipschitz-normalised weights + launch plan */
 
 typedef struct InfBroydenStats {  /* mirrors the dict returned by broyden() (broyden.py:184-193) */
-  int nstep;
-  int lowest_step;
-  int prot_break;         /* 1 => fell back to the Banach fixed point (implicit_block.py:74-75) */
+  int nstep;              /* per-sample mode: the largest per-sample nstep */
+  int lowest_step;        /* per-sample mode: the largest per-sample lowest_step */
+  int prot_break;         /* 1 => fell back to the Banach fixed point (implicit_block.py:74-75); per-sample: any */
   int n_trace;
-  double trace[64];       /* ||g||_F per iteration; trace[0] is the initial objective */
+  double trace[64];       /* ||g||_F over the batch per iteration; trace[0] is the initial objective */
   double diff;            /* ||g(result)||_F */
-  double eps;             /* eps * sqrt(B*d) (broyden.py:131) */
+  double eps;             /* eps * sqrt(B*d) (broyden.py:131); per-sample mode: eps * sqrt(d) */
   int fixed_point_iters;  /* iterations of the fallback, 0 if unused */
+  int convergence;        /* InfConvergence the solve ran with */
+  /* per-sample mode only: optional HOST arrays of `batch` ints set by the CALLER before the call (NULL: not
+   * written) that receive each sample's nstep, lowest_step and prot_break */
+  int* sample_nstep;
+  int* sample_lowest_step;
+  int* sample_prot_break;
 } InfBroydenStats;
 
 /* ---- library ------------------------------------------------------------------------------ */
@@ -87,17 +97,43 @@ int inf_net_refresh(InfNet* net, void* stream);
  *   INF_MFMA_BF16X6 both operands split exactly into three bf16 pieces (x = hi + mid + lo, truncation),
  *                   the six products down to 2^-16 relative on v_mfma_f32_32x32x16_bf16, fp32 accumulation:
  *                   dropped terms <= 2^-23 relative, i.e. fp32-level error at 16x the per-clock MFMA rate.
- *   INF_MFMA_F16X3  phases A and C as BF16X6; phase B (the HID x HID contraction) with both operands split
- *                   into two fp16 pieces after a power-of-two scale (weights: per matrix; activations: per
- *                   pixel column, from the column's max), x*S = h + l with h = rne16(x*S), l = rne16(x*S - h):
- *                   |x*S - h - l| <= 2^-24 |x*S|; three products (lh, hl, hh) on v_mfma_f32_32x32x16_f16,
- *                   fp32 accumulation, unscaled exactly (ldexp) in the epilogue: fp32-level error at
- *                   twice the BF16X6 product rate, 4 instead of 6 operand bytes per weight.
- * Default: INFLOW_MFMA=f32 / bf16x6 / f16x3 in the environment at inf_net_create, otherwise F16X3.
+ *   INF_MFMA_F16X3  all three contractions with both operands split into two fp16 pieces after a power-of-two
+ *                   scale S (weights: per matrix; activations: per pixel column in phases B and C, per tile in
+ *                   phase A, from that set's max m, so m*S is in [2^14, 2^15)): x*S = h + l with h = rne16(x*S),
+ *                   l = rne16(x*S - h): |x*S - h - l| <= 2^-23 |x*S| while l is a normal fp16
+ *                   (|x*S - h| >= 2^-14), <= 2^-25 absolute below that; relative to the set, <= 2^-23 m*S
+ *                   for every element (small entries get an absolute, not a relative, bound).  Three products (lh, hl, hh) on
+ *                   v_mfma_f32_32x32x16_f16, fp32 accumulation, unscaled exactly (ldexp): fp32-level error of
+ *                   each dot product at twice the BF16X6 product rate, 4 instead of 6 operand bytes per weight.
+ * Default: INFLOW_MFMA=f32 (or fp32) / bf16x6 / f16x3 in the environment at inf_net_create, otherwise F16X3; any
+ * other value makes inf_net_create fail with INF_ERR_INVALID.
  * No effect on nets outside the fused path. */
 typedef enum InfMfmaMode { INF_MFMA_F32 = 0, INF_MFMA_BF16X6 = 1, INF_MFMA_F16X3 = 2 } InfMfmaMode;
 int inf_net_set_mfma(InfNet* net, int mode);
 int inf_net_get_mfma(const InfNet* net);
+/* Per-net options (no process-wide switches: two threads driving different nets never share one).  Returns the
+ * previous value, or -INF_ERR_INVALID for an unknown option or a value out of range.
+ *   INF_OPT_FUSED_K128    which kernel runs the fused VJP and forward (EVAL) of 512-wide nets in INF_MFMA_F16X3:
+ *                         0 the 64-pixel kernel only; 1 the 128-pixel K-chunked kernel where its grid still covers
+ *                         all 256 CUs (default, or INFLOW_FUSED_K128 at inf_net_create); 2 wherever its tile fits.
+ *                         A paired launch (both branches of an imBlock) follows the first net's value.
+ *   INF_OPT_EVAL_OVERLAP  read on net_x of inf_imblock_eval: 1 (default; INFLOW_EVAL_OVERLAP=0 at create for 0) runs
+ *                         the x-branch series on a side stream beside the root solve and the z-branch series (the
+ *                         streams join before the call returns; needs workspace for a third region); 0 runs both
+ *                         series in lockstep on the caller's stream.  Results agree to fp32 roundoff.
+ *   INF_OPT_CONVERGENCE   read on the net whose root is solved (nnet_z forward, nnet_x inverse): INF_CONV_GLOBAL
+ *                         (default) is the reference's rule, one Frobenius norm over the batch against
+ *                         eps sqrt(B d) and one lowest iterate for the batch (broyden.py:131,153-163); with
+ *                         INF_CONV_PER_SAMPLE each sample stops on its own norm against eps sqrt(d) with its own
+ *                         lowest iterate, stall and protective breaks and Banach fallback -- the reference's result
+ *                         for a batch of one, so a sharded batch gives the single-process result row for row.
+ *                         INFLOW_CONVERGENCE=per_sample at create selects it.
+ * Performance knobs 0/1/2 of FUSED_K128 and EVAL_OVERLAP have no reference counterpart (the reference runs the VJP
+ * as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322). */
+typedef enum InfNetOption { INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3 } InfNetOption;
+typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
+int inf_net_set_option(InfNet* net, int option, int value);
+int inf_net_get_option(const InfNet* net, int option);
 /* Workspace for any call below on a net of this shape at this batch size. */
 size_t inf_workspace_bytes(const InfNet* net, int batch, int threshold);
 /* y = nnet(x). */
@@ -113,6 +149,12 @@ int inf_net_vjp(InfNet* net, const float* x, const float* v, float* out, int bat
  * may be NULL) receives the per-sample residual norms of the returned iterate. */
 int inf_root_find(InfNet* net_f, InfNet* net_e, const float* y, float* out, int batch, int threshold, double eps,
                   InfBroydenStats* stats, float* diff_detail, void* ws, size_t ws_bytes, void* stream);
+/* RootFind with method 'banach' (implicit_block.py:57-65, 83-87): x_embed = e(y) + y, then find_fixed_point
+ * (:17-28) of out <- x_embed - f(out) from out = y: stop once (out - out_prev)^2 / (eps + eps |y|) < 1 everywhere
+ * (INF_CONV_PER_SAMPLE on net_f: per sample), or after more than `threshold` iterations.  iters (HOST, may be
+ * NULL) receives the iteration count.  ws >= inf_workspace_bytes(net_f, batch, 1). */
+int inf_banach_find_root(InfNet* net_f, InfNet* net_e, const float* y, float* out, int batch, int threshold,
+                         double eps, int* iters, void* ws, size_t ws_bytes, void* stream);
 /* One limited-memory Broyden update for a caller-driven loop (generic broyden(g, x0, ...), broyden.py:
  * 174-181 + the next line_search step :94-99).  Tensors are (B, d) row-major; U/VT are (T, B, d).
  * nstep = iterations done so far (>= 1).  Writes update = -H gx, x_next = x + update and
@@ -144,7 +186,8 @@ int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_
  * only the z-net needs its own.  INF_ERR_UNSUPPORTED when a net is not fused (use the separate calls).
  * ws >= inf_workspace_bytes(net_x, batch, threshold) + inf_workspace_bytes(net_z, batch, 1).  With a further
  * inf_workspace_bytes(net_x, batch, 1) the x-branch series runs on an internal side stream concurrently with
- * the root solve and the z-branch series (joined into `stream` before return) when INFLOW_EVAL_OVERLAP=1 (off by default). */
+ * the root solve and the z-branch series (joined into `stream` before return) when net_x's INF_OPT_EVAL_OVERLAP is 1
+ * (the default). */
 int inf_imblock_eval(InfNet* net_x, InfNet* net_z, const float* x, float* z, const float* eps_x, const float* eps_z,
                      const float* coeff, int n_terms, float* logdet_x, float* logdet_z, int batch, int threshold,
                      double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
@@ -192,7 +235,8 @@ int inf_normal_logprob(const float* z, float* out, int batch, int per_sample, vo
  * draws probes on the host, implicit_block.py:297-298). */
 int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* stream);
 
-/* ---- measurement: opt-in per-launch timing with HIP events (not re-entrant; off by default) ---- */
+/* ---- measurement: opt-in per-launch timing with HIP events (off by default).  A session is per host thread:
+ * it records the launches made by the thread that called inf_profile_begin. ---- */
 typedef struct InfKernelStat {
   int tag;          /* kernel instantiation id ("Kernel tags") */
   int launches;
@@ -254,22 +298,6 @@ int inf_net_surrogate_grad(InfNet* net, const float* x, const float* w, const fl
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);
-/* Which kernel runs the fused VJP and forward (EVAL) of 512-wide nets in INF_MFMA_F16X3 (process-wide; fused313k.hip):
- *   0  the 64-pixel kernel only;
- *   1  the 128-pixel K-chunked kernel where its grid still covers all 256 CUs (default, or INFLOW_FUSED_K128);
- *   2  the 128-pixel kernel wherever its tile fits (parity tests at small batch).
- * Returns the previous policy, or -INF_ERR_INVALID for a policy outside 0..2.  No reference counterpart:
- * a performance knob of this build (the reference runs the VJP as autograd, implicit_block.py:418-426, and the
- * forward as three F.conv2d calls, mixed_lipschitz.py:388-391). */
-int inf_set_fused_k128(int policy);
-/* Eval schedule of inf_imblock_eval (process-wide): 1 (default, or INFLOW_EVAL_OVERLAP=0 in the environment for 0)
- * runs the x-branch log-det series on a side stream beside the root solve and the z-branch series (the streams
- * join before the call returns; needs workspace for a third region, otherwise the call runs sequentially);
- * 0 runs both series in lockstep on the caller's stream.  Results agree to fp32 roundoff (a per-net launch may
- * pick another tile variant than the pair's, i.e. another summation order).  Returns the previous value, or
- * -INF_ERR_INVALID.  No reference counterpart (the reference evaluates the two series one after the other,
- * implicit_block.py:300-322). */
-int inf_set_eval_overlap(int on);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,211 @@
+"""Reference parity of the paths around the eval hot path (golden vectors from the reference itself,
+tests/golden/make_golden_edges.py):
+
+  * f2  Lipschitz power iteration, compute_weight(update=True) (mixed_lipschitz.py:85-124,276-386) on the CIFAR /
+        POWER layer shapes: iteration count exact, sigma within 1e-5 relative, u / v within 1e-5 (summaries: 1e-4);
+  * f3  ImplicitFlow.inverse(z, logpz) -> imBlock.inverse (implicit_flow.py:221-251, implicit_block.py:236-243):
+        per-block Broyden steps and series lengths exact, x within 2e-4, log p within 2e-3 nats;
+  * a17 iResBlock in eval (iresblock.py:54-164): 20 exact terms + Gaussian probes, the d == 2 determinant, a conv net;
+        forward and inverse (fixed point) with their log-dets;
+  * a3  RootFind 'banach' (find_fixed_point, implicit_block.py:17-28,57-65), batch-wide and per sample;
+  * a4  Broyden stopping at the threshold and at the stall break (broyden.py:153-168), and the NaN scrub of a
+        degenerate v^T dg (:177-178): one sample with g(0) == 0 exactly.
+Tolerances are the ones of test_gpu_parity.py (fp32, reordered sums)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from lib import _hip, synthetic as syn
+from lib.configs import build_flow, imblocks
+from lib.density import image_logpx
+from lib.layers import RootFind, iResBlock, set_probe_mode
+from lib.layers.base import InducedNormConv2d, Sin, Swish, get_linear
+from lib.layers.base import lipschitz_ops as lo
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def _golden(golden_dir, name):
+    path = os.path.join(golden_dir, name + '.npz')
+    if not os.path.exists(path):
+        pytest.skip('missing fixture ' + name)
+    return np.load(path)
+
+
+def _model(arch, B):
+    m = build_flow(arch, B)
+    m.load_state_dict(syn.make_state_dict(arch, 0), strict=True)
+    return m.to(DEV).eval()
+
+
+def _check_vec(g, key, got, atol=1e-5):
+    got = got.detach().double().cpu().numpy().ravel()
+    if key in g:
+        np.testing.assert_allclose(got, g[key], rtol=0, atol=atol, err_msg=key)
+        return
+    sums, head = syn.vec_summary(got, key)
+    ref_sums = g[key + ':sum']
+    np.testing.assert_allclose(head, g[key + ':head'], rtol=0, atol=atol, err_msg=key)
+    np.testing.assert_allclose(sums, ref_sums, rtol=1e-4, atol=1e-4, err_msg=key)
+
+
+def test_power_iteration_matches_reference(golden_dir):
+    g = _golden(golden_dir, 'power_iter_layers')
+    sds = {a: syn.make_state_dict(syn.CONFIGS[a], 0) for a in ('cifar10', 'power')}
+    for i, (arch, key, kind, cin, cout, k, hw, n_it, pert) in enumerate(syn.POWER_ITER_LAYERS):
+        sd = sds[arch]
+        coeff = syn.CONFIGS[arch]['coeff']
+        if kind == 'conv':
+            m = lo.InducedNormConv2d(cin, cout, k, 1, k // 2, coeff=coeff, atol=1e-3, rtol=1e-3)
+            names = ('initialized', 'spatial_dims', 'scale', 'u', 'v')
+        else:
+            m = lo.InducedNormLinear(cin, cout, coeff=coeff, atol=1e-3, rtol=1e-3)
+            names = ('scale', 'u', 'v')
+        for name in names:
+            setattr(m, name, sd[key + '.' + name].clone())
+        with torch.no_grad():
+            m.weight.copy_(syn.perturbed_weight(sd, key, scale=pert))
+            m.bias.copy_(sd[key + '.bias'])
+        m = m.to(DEV)
+        with torch.no_grad():
+            w_eff = m.compute_weight(update=True, n_iterations=n_it)
+        torch.cuda.synchronize()
+        p = 'L%d' % i
+        assert m.last_power_iters == int(g[p + ':iters']), (key, m.last_power_iters, int(g[p + ':iters']))
+        assert abs(m.scale.item() - float(g[p + ':scale'])) <= 1e-5 * abs(float(g[p + ':scale'])), key
+        _check_vec(g, p + ':u', m.u)
+        _check_vec(g, p + ':v', m.v)
+        assert abs(w_eff.double().sum().item() - float(g[p + ':weff_sum'])) <= 1e-4 * max(1., abs(float(
+            g[p + ':weff_sum']))), key
+
+
+@pytest.mark.parametrize('name,arch', [('inverse_small_b4', syn.CIFAR10_SMALL), ('inverse_full_b2', syn.CIFAR10)])
+def test_flow_inverse_matches_reference(golden_dir, name, arch):
+    g = _golden(golden_dir, name)
+    z = torch.from_numpy(g['z']).to(DEV)
+    B = z.shape[0]
+    m = _model(arch, B)
+    set_probe_mode('reference')
+    seed = int(g['seed'])
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        x, logpz = m.inverse(z, torch.zeros(B, 1, device=DEV))
+    torch.cuda.synchronize()
+    blocks = imblocks(m)[::-1]                         # the inverse runs the blocks last to first
+    assert len(blocks) == int(g['nblocks'])
+    for i, b in enumerate(blocks):
+        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]), i
+        assert b.last_broyden['lowest_step'] == int(g['b%d_lowest_step' % i]), i
+        assert b.last_n_power_series == int(g['b%d_n_power_series' % i][0]), i
+    np.testing.assert_allclose(x.reshape(B, -1).cpu().numpy(), g['x'], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(logpz.view(-1).cpu().numpy(), g['logpz'], rtol=0, atol=2e-3)
+
+
+def _ires_net(kind):
+    if kind == 'conv':
+        conv = lambda a, b, k: InducedNormConv2d(a, b, k, 1, k // 2, coeff=0.97, atol=1e-3, rtol=1e-3)
+        return torch.nn.Sequential(conv(12, 64, 3), Swish(), conv(64, 64, 1), Swish(), conv(64, 12, 3))
+    d = 6 if kind == 'fc' else 2
+    lin = lambda a, b: get_linear(a, b, coeff=0.97, n_iterations=None, atol=1e-3, rtol=1e-3, domain=2, codomain=2)
+    return torch.nn.Sequential(lin(d, 64), Sin(), lin(64, 64), Sin(), lin(64, d))
+
+
+@pytest.mark.parametrize('name,kind', [('ires_eval_fc_b64', 'fc'), ('ires_eval_toy_b64', 'toy'),
+                                       ('ires_eval_conv_b2', 'conv')])
+def test_iresblock_eval_matches_reference(golden_dir, name, kind):
+    g = _golden(golden_dir, name)
+    blk = iResBlock(_ires_net(kind), n_dist='geometric', n_exact_terms=2, neumann_grad=True, grad_in_forward=False,
+                    brute_force=False)
+    sd = {k[3:]: torch.from_numpy(np.asarray(g[k])) for k in g.files if k.startswith('sd:')}
+    blk.load_state_dict(sd, strict=True)
+    blk = blk.to(DEV).eval()
+    x = torch.from_numpy(g['x']).to(DEV)
+    B = x.shape[0]
+    set_probe_mode('reference')
+    seed = int(g['seed'])
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        y, logpy = blk(x, torch.zeros(B, 1, device=DEV))
+        xr, logpx = blk.inverse(y, torch.zeros(B, 1, device=DEV))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(y.cpu().numpy(), g['y'], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(logpy.view(-1).cpu().numpy(), g['logpy'], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(xr.cpu().numpy(), g['xr'], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=0, atol=2e-3)
+
+
+@pytest.mark.parametrize('per_sample', [False, True])
+def test_banach_root_find_matches_reference(golden_dir, per_sample):
+    g = _golden(golden_dir, 'banach_b2')
+    x = torch.from_numpy(g['x']).to(DEV)
+    m = _model(syn.CIFAR10, x.shape[0])
+    blk = imblocks(m)[1]
+    blk(x[:1])                                       # builds the engine nets
+    nets = [n for net in (blk.nnet_x, blk.nnet_z) for n in net.__dict__['_inf_native'].values()]
+    for n in nets:
+        n.set_option(_hip.INF_OPT_CONVERGENCE, _hip.INF_CONV_PER_SAMPLE if per_sample else _hip.INF_CONV_GLOBAL)
+    try:
+        with torch.no_grad():
+            z = RootFind.apply(blk.nnet_z, blk.nnet_x, x, x, 'banach', float(g['eps']), int(g['threshold']))
+        torch.cuda.synchronize()
+    finally:
+        for n in nets:
+            n.set_option(_hip.INF_OPT_CONVERGENCE, _hip.INF_CONV_GLOBAL)
+    ref, it = (g['z_ps'], int(g['iters_ps'].max())) if per_sample else (g['z'], int(g['iters']))
+    assert RootFind.last['fixed_point_iters'] == it
+    np.testing.assert_allclose(z.cpu().numpy(), ref, rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize('name', ['threshold_small_b4', 'stall_small_b4'])
+def test_broyden_threshold_and_stall_match_reference(golden_dir, name):
+    """threshold 3 with eps 1e-9 (nstep == threshold, lowest iterate returned) and threshold 1 with eps = obj_1 / 2
+    (the stall break, broyden.py:165-168, which the reference logged: 'Iterations exceeded')."""
+    g = _golden(golden_dir, name)
+    arch = syn.CIFAR10_SMALL
+    x = torch.from_numpy(g['x']).to(DEV)
+    m = _model(arch, x.shape[0])
+    for i, b in enumerate(imblocks(m)):
+        b.threshold = int(g['b%d_threshold' % i])
+        b.eps_forward = float(g['b%d_eps_forward' % i])
+    if name == 'stall_small_b4':
+        assert any('exceeded' in str(s) for s in g['log'])
+    set_probe_mode('reference')
+    np.random.seed(int(g['seed']))
+    torch.manual_seed(int(g['seed']))
+    loss, logpx, z = image_logpx(m, x, arch['nvals'])
+    torch.cuda.synchronize()
+    for i, b in enumerate(imblocks(m)):
+        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]) == b.threshold, i
+        assert b.last_broyden['lowest_step'] == int(g['b%d_lowest_step' % i]), i
+        assert not b.last_broyden['prot_break']
+    assert abs(loss.item() - float(g['loss'])) <= 1e-5
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(z.reshape(z.shape[0], -1).cpu().numpy(), g['z'], rtol=0, atol=2e-4)
+
+
+def test_degenerate_broyden_update_matches_reference(golden_dir):
+    """nnet_z = nnet_x and a zero sample: g(0) == 0 for that sample in the reference, so v^T dg == 0 and
+    u = 0 / 0 is scrubbed to 0 (broyden.py:177-178); the engine's f(0) may differ in the last bit, so the sample
+    solves a tiny system instead -- either way z == 0 for it and the batch matches."""
+    g = _golden(golden_dir, 'degenerate_small_b4')
+    x = torch.from_numpy(g['x']).to(DEV)
+    B = x.shape[0]
+    m = _model(syn.CIFAR10_SMALL, B)
+    blk = imblocks(m)[0]
+    blk.nnet_z.load_state_dict(blk.nnet_x.state_dict())
+    set_probe_mode('reference')
+    np.random.seed(int(g['seed']))
+    torch.manual_seed(int(g['seed']))
+    with torch.no_grad():
+        z, lp = blk(x, torch.zeros(B, 1, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.isfinite(z).all() and torch.isfinite(lp).all()
+    assert blk.last_broyden['nstep'] == int(g['nstep'])
+    assert z[0].abs().max().item() <= 1e-6
+    np.testing.assert_allclose(z.cpu().numpy(), g['z'], rtol=0, atol=2e-4)
+    np.testing.assert_allclose((-lp).view(-1).cpu().numpy(), g['logdet'], rtol=0, atol=2e-3)

@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from lib import _hip, synthetic as syn
-from lib.configs import build_flow, imblocks
+from lib.configs import build_flow, engine_nets, imblocks, restore_engine_options, set_engine_option
 from lib.density import image_logpx, tabular_logpx
 from lib.layers import solvers
 from oracle import inflow_oracle as orc
@@ -152,6 +152,56 @@ def test_flow_matches_reference_golden(golden_dir, name, arch, train):
     np.testing.assert_allclose(z.reshape(z.shape[0], -1).cpu().numpy(), g['z'], rtol=0, atol=2e-4)
 
 
+def test_headline_b64_matches_reference_golden(golden_dir):
+    """The bench configuration itself (BASELINE.json configs[2]: run_cifar10.sh model, eval, B=64) on the exact timed
+    path -- the default per-net options (128-pixel K-chunked VJP and EVAL kernels, overlapped x-branch series, f16x3
+    MFMA, fast-sigmoid epilogues) -- against the reference's own run on the same inputs and seeds
+    (tests/golden/make_golden.py cifar_full_b64), with the reference's probe stream replayed.  Per imBlock: Broyden
+    nstep / lowest_step and the series length exact, the per-sample sum of the block output z within 2e-3 and the
+    per-sample log-det within 2e-3 nats; bits/dim within 1e-5; per-sample log p within 2e-3 nats; z within 2e-4."""
+    g = _golden(golden_dir, 'cifar_full_b64')
+    arch = syn.CIFAR10
+    x = torch.from_numpy(g['x']).to(DEV)
+    m, _ = _model(arch, x.shape[0])
+    rec = []
+
+    def hook(mod, args, kwargs, out):
+        lp_in = args[1] if len(args) > 1 else kwargs.get('logpx')
+        z, lp_out = out
+        rec.append((z.detach().reshape(z.shape[0], -1).double().sum(1).cpu(),
+                    (lp_in - lp_out).detach().view(-1).cpu()))
+    hooks = [b.register_forward_hook(hook, with_kwargs=True) for b in imblocks(m)]
+    np.random.seed(int(g['seed']))
+    torch.manual_seed(int(g['seed']))
+    _hip.profile_begin(20000)
+    try:
+        loss, logpx, z = image_logpx(m, x, arch['nvals'])
+        torch.cuda.synchronize()
+    finally:
+        stats = _hip.profile_end()
+        for h in hooks:
+            h.remove()
+    # the default path of the bench: f16x3, per-net options at their defaults, the 128-pixel kernels used
+    nets = engine_nets(m)
+    assert nets and all(n.lib.inf_net_get_mfma(n.handle) == 2 for n in nets)
+    assert all(n.get_option(_hip.INF_OPT_FUSED_K128) == 1 and n.get_option(_hip.INF_OPT_EVAL_OVERLAP) == 1
+               for n in nets)
+    tags = {s_['tag'] for s_ in stats}
+    assert 532 in tags and 530 in tags, sorted(tags)          # net313k_kernel<VJP>, net313k_kernel<EVAL>
+    blocks = imblocks(m)
+    assert len(rec) == len(blocks) == int(g['nblocks'])
+    for i, b in enumerate(blocks):
+        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]), 'block %d nstep' % i
+        assert b.last_broyden['lowest_step'] == int(g['b%d_lowest_step' % i]), 'block %d lowest_step' % i
+        assert b.last_n_power_series == int(g['b%d_n_power_series' % i][0]), 'block %d n_ps' % i
+        np.testing.assert_allclose(rec[i][0].numpy(), g['b%d_zsum' % i], rtol=0, atol=2e-3)
+        np.testing.assert_allclose(rec[i][1].numpy(), g['b%d_logdet' % i], rtol=0, atol=2e-3)
+    print('bpd %.8f ref %.8f  |d| %.2e' % (loss.item(), float(g['loss']), abs(loss.item() - float(g['loss']))))
+    assert abs(loss.item() - float(g['loss'])) <= 1e-5
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(z.reshape(z.shape[0], -1).cpu().numpy(), g['z'], rtol=0, atol=2e-4)
+
+
 def test_flow_matches_oracle_small_batch():
     arch = syn.CIFAR10_SMALL
     x = syn.image_batch(5, seed=9)
@@ -167,9 +217,9 @@ def test_flow_matches_oracle_small_batch():
     np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), ref_logpx.view(-1).numpy(), rtol=0, atol=2e-3)
 
 
-def test_deterministic_and_shard_invariant():
-    """Same inputs -> bitwise same bpd; per-sample logpx of a half batch equals the full batch's rows
-    when the probes are the same (Broyden's global stop can differ only below eps)."""
+def test_deterministic_repeat():
+    """Same inputs, seeds and probes -> bitwise the same per-sample log p (no nondeterministic reduction on the
+    path).  Shard invariance is test_per_sample_shards_match_full_batch / test_two_rank_sharded_eval."""
     arch = syn.CIFAR10_SMALL
     x = syn.image_batch(4, seed=1).to(DEV)
     m, _ = _model(arch, 4)
@@ -287,15 +337,16 @@ def test_fused_313_matches_generic_path(block, B, mfma, monkeypatch):
         _close(a, b, rel=1e-5)
 
 
-@pytest.mark.parametrize('block', [0, 1, 2, 4])
-def test_split_bf16_error_at_fp32_level(block):
+@pytest.mark.parametrize('block,B,k128', [(0, 4, 1), (1, 4, 1), (2, 4, 1), (4, 4, 1), (0, 64, 1), (2, 64, 2)])
+def test_split_bf16_error_at_fp32_level(block, B, k128):
     """INF_MFMA_BF16X6 (exact three-way bf16 split, six products per fp32 product) against INF_MFMA_F32 on the
     full-size CIFAR nets: both forward and VJP measured against an fp64 CPU evaluation of the same net.
     Tolerance: the split path's max error (relative to max|ref|) <= 1.5x the fp32 MFMA path's + 1e-7,
     and both <= 2e-6 (fp32 roundoff level).  INF_MFMA_F16X3 (scaled two-piece fp16 phase B, three products):
-    <= 2x the fp32 MFMA path's + 2e-7, and <= 2e-6."""
+    <= 2x the fp32 MFMA path's + 2e-7, and <= 2e-6.  B=4 takes the 32-pixel tiles; B=64 the bench's kernels: the
+    128-pixel K-chunked VJP / forward at s0 (its default policy there) and forced at s1 (INF_OPT_FUSED_K128 = 2),
+    checked to have run."""
     arch = syn.CIFAR10
-    B = 4
     m, sd = _model(arch, B)
     blk = imblocks(m)[block]
     prefix, info = _first_block_net(arch, sd, block=block)
@@ -312,23 +363,37 @@ def test_split_bf16_error_at_fp32_level(block):
     stream = _hip.stream_of(xd)
     net.refresh_if_needed(stream)
     ws = _hip.workspace(xd.device, net.ws_bytes(B))
+    k_prev = net.set_option(_hip.INF_OPT_FUSED_K128, k128)
     err = {}
-    for mode in (0, 1, 2):
-        _hip.check(net.lib.inf_net_set_mfma(net.handle, mode), 'set_mfma')
-        assert net.lib.inf_net_get_mfma(net.handle) == mode
-        y = torch.empty_like(xd)
-        g = torch.empty_like(xd)
-        _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(xd), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
-                                           stream), 'fwd')
-        _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(xd), _hip.ptr(vd), _hip.ptr(g), B, _hip.ptr(ws),
-                                       ws.numel(), stream), 'vjp')
-        torch.cuda.synchronize()
-        err[mode] = [((a.double().cpu() - r).abs().max() / r.abs().max()).item() for a, r in ((y, y_ref), (g, g_ref))]
+    try:
+        _run_error_modes(net, xd, vd, B, ws, stream, y_ref, g_ref, err, expect_k128=(B == 64))
+    finally:
+        net.set_option(_hip.INF_OPT_FUSED_K128, k_prev)
     print('max error vs fp64 (fwd, vjp): f32 %s  bf16x6 %s  f16x3 %s' % (err[0], err[1], err[2]))
     for e32, e6, e3 in zip(err[0], err[1], err[2]):
         assert e32 <= 2e-6 and e6 <= 2e-6 and e3 <= 2e-6, err
         assert e6 <= 1.5 * e32 + 1e-7, err
         assert e3 <= 2.0 * e32 + 2e-7, err
+
+
+def _run_error_modes(net, xd, vd, B, ws, stream, y_ref, g_ref, err, expect_k128):
+    for mode in (0, 1, 2):
+        _hip.check(net.lib.inf_net_set_mfma(net.handle, mode), 'set_mfma')
+        assert net.lib.inf_net_get_mfma(net.handle) == mode
+        y = torch.empty_like(xd)
+        g = torch.empty_like(xd)
+        _hip.profile_begin(100)
+        try:
+            _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(xd), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
+                                               stream), 'fwd')
+            _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(xd), _hip.ptr(vd), _hip.ptr(g), B, _hip.ptr(ws),
+                                           ws.numel(), stream), 'vjp')
+            torch.cuda.synchronize()
+        finally:
+            tags = {s_['tag'] for s_ in _hip.profile_end()}
+        if mode == 2 and expect_k128:
+            assert 532 in tags and 530 in tags, sorted(tags)    # net313k_kernel<VJP>, <EVAL>
+        err[mode] = [((a.double().cpu() - r).abs().max() / r.abs().max()).item() for a, r in ((y, y_ref), (g, g_ref))]
 
 
 @pytest.mark.parametrize('kind', ['conv3', 'conv1', 'linear', 'conv3_fixed', 'conv3_cifar'])
@@ -481,9 +546,10 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B):
         ws.fill_(255)
         _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
     outs = {}
+    k_prev = net.get_option(_hip.INF_OPT_FUSED_K128)
     try:
         for pol in (2, 0):
-            prev = net.lib.inf_set_fused_k128(pol)
+            prev = net.set_option(_hip.INF_OPT_FUSED_K128, pol)
             assert prev in (0, 1, 2)
             y, g, ld, w = torch.empty_like(x), torch.empty_like(x), torch.empty(B, device=DEV), torch.empty_like(x)
             poison()
@@ -501,8 +567,9 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B):
             torch.cuda.synchronize()
             outs[pol] = (y, g, ld, w)
     finally:
-        net.lib.inf_set_fused_k128(1)
-    assert net.lib.inf_set_fused_k128(3) < 0
+        net.set_option(_hip.INF_OPT_FUSED_K128, k_prev)
+    assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_K128, 3) < 0
+    assert net.get_option(_hip.INF_OPT_FUSED_K128) == k_prev
     for a in outs[2]:
         assert torch.isfinite(a).all()
     for a, b in zip(outs[2], outs[0]):
@@ -518,12 +585,13 @@ def test_eval_overlap_matches_sequential():
     B = 64
     m, _ = _model(arch, B)
     x = syn.image_batch(B, seed=21).to(DEV)
-    lib = _hip.load()
+    image_logpx(m, x, arch['nvals'])                   # creates the engine nets
     res = {}
+    prev = None
     try:
         for ov in (1, 0):
-            prev = lib.inf_set_eval_overlap(ov)
-            assert prev in (0, 1)
+            p = set_engine_option(m, _hip.INF_OPT_EVAL_OVERLAP, ov)
+            prev = prev or p
             np.random.seed(5)
             torch.manual_seed(5)
             bpd, logpx, _ = image_logpx(m, x, arch['nvals'])
@@ -531,8 +599,10 @@ def test_eval_overlap_matches_sequential():
             res[ov] = (bpd.item(), logpx.detach().cpu(), [b.last_broyden['nstep'] for b in imblocks(m)],
                        [b.last_n_power_series for b in imblocks(m)])
     finally:
-        lib.inf_set_eval_overlap(1)
-    assert lib.inf_set_eval_overlap(2) < 0
+        if prev:
+            restore_engine_options(_hip.INF_OPT_EVAL_OVERLAP, prev)
+    n0 = engine_nets(m)[0]
+    assert n0.lib.inf_net_set_option(n0.handle, _hip.INF_OPT_EVAL_OVERLAP, 2) < 0
     assert res[1][2] == res[0][2] and res[1][3] == res[0][3]
     assert abs(res[1][0] - res[0][0]) <= 1e-5
     np.testing.assert_allclose(res[1][1].numpy(), res[0][1].numpy(), rtol=0, atol=2e-3)

@@ -36,21 +36,40 @@ def test_binding_signatures_cover_header():
     assert set(_declared_symbols()) == set(_hip.EXPORTS)
 
 
-def test_process_wide_schedule_switches():
-    """inf_set_fused_k128 (0 / 1 / 2) and inf_set_eval_overlap (0 / 1) return the previous value and reject
-    anything else with -INF_ERR_INVALID, leaving the setting unchanged (host-only: no GPU call)."""
+def test_no_process_wide_switches():
+    """Every schedule / semantics switch is a per-net option (no mutable globals in the .so): the old
+    process-wide setters are gone, and inf_net_set_option / inf_net_get_option reject a null net with
+    -INF_ERR_INVALID (host-only: no GPU call)."""
     if not os.path.exists(_hip.LIB_PATH):
         pytest.skip('libinflow.so not built (run __graft_entry__.build())')
+    lib = ctypes.CDLL(_hip.LIB_PATH)
+    assert not hasattr(lib, 'inf_set_fused_k128') and not hasattr(lib, 'inf_set_eval_overlap')
     lib = _hip.load()
-    k0 = lib.inf_set_fused_k128(2)
-    assert k0 in (0, 1, 2)
-    assert lib.inf_set_fused_k128(7) == -1 and lib.inf_set_fused_k128(-1) == -1
-    assert lib.inf_set_fused_k128(0) == 2
-    assert lib.inf_set_fused_k128(k0) == 0
-    o0 = lib.inf_set_eval_overlap(0)
-    assert o0 in (0, 1)
-    assert lib.inf_set_eval_overlap(2) == -1
-    assert lib.inf_set_eval_overlap(o0) == 0
+    for opt in (_hip.INF_OPT_FUSED_K128, _hip.INF_OPT_EVAL_OVERLAP, _hip.INF_OPT_CONVERGENCE):
+        assert lib.inf_net_set_option(None, opt, 0) == -1
+        assert lib.inf_net_get_option(None, opt) == -1
+
+
+def test_sharded_probes_are_rows_of_the_global_draw():
+    """set_probe_shard: each shard's Rademacher probes are its rows of the probes the single-process run draws for
+    the whole batch, in the reference's order (vareps_x then vareps_z, implicit_block.py:297-298), so a sharded
+    evaluation sees the same probes per sample."""
+    from lib.layers import imblock as ib
+    shape = (7, 3, 4, 4)
+    torch.manual_seed(11)
+    ib.set_probe_mode('reference')
+    full = [ib._probes(shape, 'cpu') for _ in range(3)]
+    try:
+        for lo, hi in ((0, 3), (3, 7), (2, 5)):
+            torch.manual_seed(11)
+            ib.set_probe_shard(lo, hi, 7)
+            part = [ib._probes((hi - lo,) + shape[1:], 'cpu') for _ in range(3)]
+            for a, b in zip(part, full):
+                assert torch.equal(a, b[lo:hi])
+        with pytest.raises(ValueError):
+            ib._probes((2,) + shape[1:], 'cpu')         # shard [2, 5) needs 3 rows
+    finally:
+        ib.set_probe_shard()
 
 
 @pytest.mark.parametrize('dist,param,n_exact', [('poisson', 2.0, 20), ('geometric', 0.5, 2), ('poisson', 2.0, 10)])
