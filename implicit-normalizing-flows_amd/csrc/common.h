@@ -33,7 +33,8 @@ __device__ __forceinline__ float swish_d(float a, float sp) {
 // two IEEE divisions and range-reduced expf were most of the VALU of the EVAL / SAVE launches: v_exp_f32 and
 // v_rcp_f32 (relative error of sigmoid <= ~1e-6 for |a sp| <= 16, against the fused kernels' 1e-5 parity bound), the
 // division by 1.1 as a multiply.  The generic GEMM path, conv_out and the gradients keep the precise forms.
-__device__ __forceinline__ float sigmoid_fast(float z) { return __frcp_rn(1.f + __expf(-z)); }
+// (__builtin_amdgcn_rcpf is the bare v_rcp_f32, 1 ulp; __frcp_rn expands to the correctly rounded division sequence)
+__device__ __forceinline__ float sigmoid_fast(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 __device__ __forceinline__ float swish_fast_f(float a, float sp) { return a * sigmoid_fast(a * sp) * (1.f / 1.1f); }
 __device__ __forceinline__ float swish_fast_d(float a, float sp) {
   const float s = sigmoid_fast(a * sp);
@@ -157,7 +158,10 @@ __host__ __device__ __forceinline__ int h3_scale_exp(float m) {
   int e;
   (void)frexpf(m, &e);            // m = f 2^e, f in [0.5, 1)
   const int s = 15 - e;
-  return s < -140 ? -140 : (s > 140 ? 140 : s);   // any finite fp32 max maps into [2^14, 2^15) (no fp16 overflow)
+  // 2^s must be a normal fp32 (the kernels form S = 2^s): s in [-126, 127].  Every finite max m <= 2^128 then maps into
+  // [2^14, 2^15) (no fp16 overflow); a max below 2^-112 maps below 2^15 (the pieces of such a set are relatively coarse,
+  // but the set is < 2^-112 in magnitude)
+  return s < -126 ? -126 : (s > 127 ? 127 : s);
 }
 __device__ __forceinline__ void split2h(const float (&x)[8], float S, u32x4& h, u32x4& l) {
 #pragma unroll

@@ -125,12 +125,12 @@ def fc_model(arch):
     return layers.SequentialFlow(blocks)
 
 
-def run_case(name, arch, x, seed, weight_seed=0, train=False):
+def run_case(name, arch, x, seed, weight_seed=0, train=False, power_iters=30):
     torch.manual_seed(1234)
     model = conv_model(arch, x.shape[0]) if arch['kind'] == 'conv' else fc_model(arch)
     with torch.no_grad():
         model(x[:2].clone(), restore=True)            # materialise lazy u/v, ActNorm init
-    sd = syn.make_state_dict(arch, weight_seed)
+    sd = syn.make_state_dict(arch, weight_seed, power_iters=power_iters)
     model.load_state_dict(sd, strict=True)
     model.train(train)
     REC.clear()
@@ -156,7 +156,7 @@ def run_case(name, arch, x, seed, weight_seed=0, train=False):
                train=np.int64(train), loss=np.float64(loss.item()),
                logpx=logpx.detach().view(-1).numpy().astype(np.float64),
                z=z.detach().view(x.shape[0], -1).numpy().astype(np.float32), seconds=np.float64(dt),
-               nblocks=np.int64(len(REC)))
+               nblocks=np.int64(len(REC)), power_iters=np.int64(power_iters))
     for i, r in enumerate(REC):
         for k, v in r.items():
             if k == 'z' and x.shape[0] * v[0].size >= 100000:    # large batches: per-sample sums only
@@ -184,6 +184,9 @@ CASES = {
     'cifar_full_b8': lambda: run_case('cifar_full_b8', syn.CIFAR10, syn.image_batch(8, seed=5), seed=11),
     # the headline bench configuration (BASELINE.json configs[2]: run_cifar10.sh, batch 64)
     'cifar_full_b64': lambda: run_case('cifar_full_b64', syn.CIFAR10, syn.image_batch(64, seed=0), seed=0),
+    # BASELINE.json configs[4]: CelebA-HQ 256 (5 bits, 4 scales), one image; weights with 5 power iterations as bench.py
+    'celebahq256_b1': lambda: run_case('celebahq256_b1', syn.CELEBAHQ256,
+                                       syn.image_batch(1, (3, 256, 256), 32, seed=2), seed=4, power_iters=5),
 }
 
 if __name__ == '__main__':

