@@ -111,7 +111,6 @@ struct InfNet {
   int k128 = 1;            // INF_OPT_FUSED_K128
   int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
-  int d1_recompute = 1;    // INF_OPT_D1_RECOMPUTE
 };
 
 namespace {
@@ -270,14 +269,6 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.k128 = n->k128;
   return f;
 }
-// VJP launches: the primal input x the net is linearised at, so the 128-pixel kernel can recompute d1 from it
-void set_primal(const InfNet* n, Net313Args& f, const float* x) {
-  if (!n->d1_recompute || n->mfma_mode != INF_MFMA_F16X3 || !x) return;
-  f.xf = x;
-  f.xf_beta = n->pre_beta;
-  f.A1fh = n->Fh[0];
-  f.A1f_exp = n->Fexp;
-}
 
 int run_forward(InfNet* n, const float* x, int B, Bufs& bf, int mode, const OutArgs* oa, hipStream_t s) {
   const int L = (int)n->L.size();
@@ -340,7 +331,6 @@ int run_vjp(InfNet* n, const float* v, float* vout, const float* xin, const floa
   const int L = (int)n->L.size();
   if (n->fused) {
     Net313Args f = net313_args(n, v, B, bf, true);
-    set_primal(n, f, xin);
     INF_TRY(launch_net313(f, n->fhid, MODE_VJP, s));
     OutArgs a;
     memset(&a, 0, sizeof(a));
@@ -1238,8 +1228,6 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     if (e && *e) n->k128 = std::min(std::max(atoi(e), 0), 2);
     e = getenv("INFLOW_EVAL_OVERLAP");                      // default of INF_OPT_EVAL_OVERLAP
     if (e && *e) n->eval_overlap = e[0] == '1' ? 1 : 0;
-    e = getenv("INFLOW_D1_RECOMPUTE");                      // default of INF_OPT_D1_RECOMPUTE
-    if (e && *e) n->d1_recompute = e[0] == '1' ? 1 : 0;
     e = getenv("INFLOW_CONVERGENCE");                       // default of INF_OPT_CONVERGENCE
     if (e && *e) n->convergence = !strcmp(e, "per_sample") ? INF_CONV_PER_SAMPLE : INF_CONV_GLOBAL;
   }
@@ -1499,7 +1487,6 @@ int series_fused(InfNet* const* nets, const float* const* xs, const float* const
       Bufs& bf = bfs[i];
       Net313Args& v = args[i];
       v = net313_args(n, es[i], B, bf, true);
-      set_primal(n, v, xs[i]);
       v.Y = (k % 2 == 0) ? bf.Y : bf.Y2;
       if (k > 0) {
         v.in = nullptr;
@@ -2123,7 +2110,6 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_FUSED_K128: slot = &n->k128; hi = 2; break;
     case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
-    case INF_OPT_D1_RECOMPUTE: slot = &n->d1_recompute; hi = 1; break;
     default: return -INF_ERR_INVALID;
   }
   if (value < lo || value > hi) return -INF_ERR_INVALID;
@@ -2138,7 +2124,6 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_FUSED_K128: return n->k128;
     case INF_OPT_EVAL_OVERLAP: return n->eval_overlap;
     case INF_OPT_CONVERGENCE: return n->convergence;
-    case INF_OPT_D1_RECOMPUTE: return n->d1_recompute;
     default: return -INF_ERR_INVALID;
   }
 }

@@ -66,17 +66,12 @@ int net313k_fits(int hid, int C, int H, int W) {
   if (9 * C > 256) return 0;                      // phase C: at most 8 row blocks x 4 columns = 4 jobs per wave
   const int rows = KB_BN / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
-  const long halo = (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
-  // chunk buffer | column maxima | 2 x 8 halo maxima | trace partials | koff | v halo | x halo (d1 recompute)
-  const long need = KB_CHUNK + KB_NW * KB_BN + 16 + 2 * KB_NW + k1pad + 2 * halo;
+  const long need = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
   return need <= KB_LDS;
 }
 
-// MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2)).
-// D1K > 0 (VJP): d1 recomputed from the primal input (Net313Args::xf) instead of read from HBM; D1K = K1pad / 16, the
-// recompute's K tiles as a compile-time count (2 at C = 3, 7 at C = 12), so its loop unrolls (a runtime loop there
-// made the register allocator spill across the whole epilogue).
-template <int MODE, int D1K = 0>
+// MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2))
+template <int MODE>
 __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   constexpr bool VJP = MODE == MODE_VJP;
   const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
@@ -100,17 +95,13 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   const int RH = rows + 2, CW = seg + 2;
   const int vhn = a.C * RH * CW;
   const int vhz = vhn + rows * CW;                  // zero run for the K-padding rows of phase A
-  // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] x 2 | trace partials [NW] (fp64) | koff | halo |
-  // x halo (VJP with the d1 recompute: the primal input, preact applied)
+  // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] | trace partials [NW] (fp64) | koff | halo
   u32x4* cb = reinterpret_cast<u32x4*>(smem);
   float* cmax = smem + KB_CHUNK;
   float* hmax = cmax + KB_NW * KB_BN;
-  float* hmaxx = hmax + 8;
-  double* red = reinterpret_cast<double*>(hmax + 16);
+  double* red = reinterpret_cast<double*>(hmax + 8);
   int* koff = reinterpret_cast<int*>(red + KB_NW);
   float* vh = reinterpret_cast<float*>(koff + a.K1pad);
-  float* xh = vh + vhz;
-  constexpr bool d1rc = VJP && D1K > 0;
 
   // d1 / d2 in the 64-pixel kernel's fragment order: 64-px tile (2 tile + b / 2), column (b & 1), row block rb
   const long tile64 = (long)img * (P / 64) + 2 * tile;
@@ -216,27 +207,6 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
         vh[i] = v;
       }
     }
-  }
-  if constexpr (d1rc) {                             // primal halo for the d1 recompute (forward staging)
-    const float* xin = a.xf + (long)img * a.C * P;
-    const float xsp = a.xf_beta ? softplus_f(*a.xf_beta) : 0.f;
-    float xmx = 0.f;
-    for (int i = tid; i < vhz; i += KB_NT) {
-      float v = 0.f;
-      if (i < vhn) {
-        const int c = i / (RH * CW), rr = i - c * RH * CW;
-        const int hy = rr / CW, hx = rr - hy * CW;
-        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-          v = xin[(long)c * P + yy * a.W + xx];
-          if (a.xf_beta) v = swish_fast_f(v, xsp);
-        }
-      }
-      xmx = fmaxf(xmx, fabsf(v));
-      xh[i] = v;
-    }
-    const float w = wave_max(xmx);
-    if (lane == 0) hmaxx[wid] = w;
   }
   {
     const float w = wave_max(hmx);
@@ -457,100 +427,16 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   float cmC[KB_NB];
 #pragma unroll
   for (int b = 0; b < KB_NB; ++b) cmC[b] = 0.f;
-  // d1 per row block: its 4 column blocks' d1 requested together (64 registers), or (D1RC) recomputed from the primal
-  // halo one 32 x 32 block at a time, a1 = W1 . im2col(preact x) (K = 9C), d1 = swish'(a1 + b1) as the SAVE launch
-  // computes it, applied to the accumulator right away
-  float sAx = 1.f, sp1x = 0.f;
-  int eAx = 0;
-  if constexpr (d1rc) {
-    float m_ = 0.f;
-#pragma unroll
-    for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, hmaxx[w]);
-    const int sc = h3_scale_exp(m_);
-    sAx = __builtin_amdgcn_ldexpf(1.f, sc);
-    eAx = -(sc + a.A1f_exp[0]);
-    sp1x = softplus_f(*a.beta1);
-  }
-  const u32x4* A1fh = reinterpret_cast<const u32x4*>(a.A1fh);
-  // lane geometry re-derived here from an opaque copy of the thread id, so the compiler does not keep the recompute's
-  // addresses live (spilled) across phase B
-  int tid_e = tid;
-  if constexpr (d1rc) asm volatile("v_mov_b32 %0, %1" : "=v"(tid_e) : "v"(tid));
-  const int lane_e = tid_e & 63, li_e = lane_e & 31, lh_e = lane_e >> 5;
-  const int wid_e = __builtin_amdgcn_readfirstlane(tid_e >> 6);
-  int pix_e[KB_NB];
-#pragma unroll
-  for (int b = 0; b < KB_NB; ++b) {
-    const int n = b * 32 + li_e;
-    const int py = n / seg;
-    pix_e[b] = py * CW + (n - py * seg);
-  }
-  // D1RC: row block 1 of the accumulator waits in the (now free) chunk buffer while row block 0's d1 is recomputed,
-  // so the recompute's operands fit beside one row block (16 KiB per wave, 128 KiB in all: the chunk buffer)
-  float* stash = smem + wid * (KB_NB * 16 * 64);
-  if constexpr (d1rc) {
-    __syncthreads();                                  // every wave is done reading the phase-B chunk buffer
-#pragma unroll
-    for (int b = 0; b < KB_NB; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) stash[(b * 16 + r) * 64 + lane] = acc[1][b][r];
-  }
+  // (one row block at a time: its 4 column blocks' d1 requested together, 64 registers)
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     f32x4 d1v[KB_NB][4];
-    if constexpr (d1rc) {
-      if (m == 1) __syncthreads();                  // (orders the stash round trip)
-      const int rb1 = 2 * wid_e + m;
 #pragma unroll
-      for (int b = 0; b < KB_NB; ++b) {
-        __builtin_amdgcn_sched_barrier(0);           // one 32 x 32 block at a time (no loads hoisted across blocks)
-        f32x16 ax;
+    for (int b = 0; b < KB_NB; ++b) {
+      if constexpr (!VJP) break;
+      const f32x4* q = dptr(a.d1, 2 * wid + m, b);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ax[r] = 0.f;
-        u32x4 w0[2], w1[2];
-        ldw2(A1fh, (long)rb1 * D1K, lane_e, w0);
-        auto stepX = [&](int kt, const u32x4 (&af)[2]) {
-          const int* kp = koff + kt * 16 + lh_e * 8;
-          const int4 k0 = *reinterpret_cast<const int4*>(kp);
-          const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
-          const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-          float x[8];
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk) x[kk] = xh[ko[kk] + pix_e[b]];
-          u32x4 h, l;
-          split2h(x, sAx, h, l);
-          ax = mfma_h3(af, h, l, ax);
-        };
-#pragma unroll
-        for (int kt = 0; kt < D1K; kt += 2) {
-          const bool has1 = kt + 1 < D1K;
-          if (has1) ldw2(A1fh, (long)rb1 * D1K + kt + 1, lane_e, w1);
-          stepX(kt, w0);
-          if (kt + 2 < D1K) ldw2(A1fh, (long)rb1 * D1K + kt + 2, lane_e, w0);
-          if (has1) stepX(kt + 1, w1);
-        }
-        const int e = -(scB[b] + ew);
-        if (m == 1) {                                   // this block's accumulator back from the stash
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[1][b][r] = stash[(b * 16 + r) * 64 + lane_e];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = rb1 * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh_e;
-          const float d = swish_fast_d(__builtin_amdgcn_ldexpf(ax[r], eAx) + a.b1[row], sp1x);
-          acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], e) * d;
-          cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
-        }
-      }
-      continue;
-    } else {
-#pragma unroll
-      for (int b = 0; b < KB_NB; ++b) {
-        if constexpr (!VJP) break;
-        const f32x4* q = dptr(a.d1, 2 * wid + m, b);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];
-      }
+      for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];
     }
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
@@ -690,10 +576,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 }
 
 int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s) {
-  const int d1k = (pr.a[0].xf != nullptr && pr.a[1].xf != nullptr) ? pr.a[0].K1pad / 16 : 0;
-  if (mode == MODE_VJP && d1k == 2) hipLaunchKernelGGL((net313k_kernel<MODE_VJP, 2>), dim3(nb), dim3(KB_NT), 0, s, pr);
-  else if (mode == MODE_VJP && d1k == 7) hipLaunchKernelGGL((net313k_kernel<MODE_VJP, 7>), dim3(nb), dim3(KB_NT), 0, s, pr);
-  else if (mode == MODE_VJP) hipLaunchKernelGGL(net313k_kernel<MODE_VJP>, dim3(nb), dim3(KB_NT), 0, s, pr);
+  if (mode == MODE_VJP) hipLaunchKernelGGL(net313k_kernel<MODE_VJP>, dim3(nb), dim3(KB_NT), 0, s, pr);
   else if (mode == MODE_EVAL) hipLaunchKernelGGL(net313k_kernel<MODE_EVAL>, dim3(nb), dim3(KB_NT), 0, s, pr);
   else return INF_ERR_UNSUPPORTED;
   INF_CHECK_LAUNCH();

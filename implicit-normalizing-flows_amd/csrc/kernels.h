@@ -180,12 +180,6 @@ struct Net313Args {
   float acc_coef;         //   implicit_block.py:430-436), v the previous term's VJP after the tap sum
   int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
                           //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
-  // 128-pixel VJP only (fused313k.hip): the epilogue-B multiplier d1 = swish'(W1 . preact(xf) + b1) recomputed from
-  // the primal input instead of read from HBM (xf == nullptr: read d1)
-  const float* xf;        // primal input x (B, C, H, W) the net is linearised at
-  const float* xf_beta;   // preact swish on xf (nullptr: none)
-  const void* A1fh;       // forward phase-A operand W1 (HID x K1pad) as two scaled fp16 planes
-  const int* A1f_exp;     // its scale exponent
 };
 struct Net313Pair {
   Net313Args a[2];

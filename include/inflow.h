@@ -128,14 +128,11 @@ int inf_net_get_mfma(const InfNet* net);
  *                         lowest iterate, stall and protective breaks and Banach fallback -- the reference's result
  *                         for a batch of one, so a sharded batch gives the single-process result row for row.
  *                         INFLOW_CONVERGENCE=per_sample at create selects it.
- *   INF_OPT_D1_RECOMPUTE  the 128-pixel VJP (F16X3) recomputes its epilogue multiplier d1 = swish'(W1 preact(x) + b1)
- *                         from the primal input x (a K = 9C contraction per tile) instead of reading the saved d1
- *                         (HID floats per pixel) from HBM: 1 (default; INFLOW_D1_RECOMPUTE=0 at create for 0) or 0.
- * FUSED_K128, EVAL_OVERLAP and D1_RECOMPUTE are performance knobs without a reference counterpart (the reference
+ * FUSED_K128 and EVAL_OVERLAP are performance knobs without a reference counterpart (the reference
  * runs the VJP as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322); results
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
-  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_D1_RECOMPUTE = 4
+  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);

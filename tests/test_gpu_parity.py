@@ -24,8 +24,8 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda:0'
 
 
-def _model(arch, B):
-    sd = syn.make_state_dict(arch, 0)
+def _model(arch, B, power_iters=30):
+    sd = syn.make_state_dict(arch, 0, power_iters=power_iters)
     m = build_flow(arch, B)
     m.load_state_dict(sd, strict=True)
     return m.to(DEV).eval(), sd
@@ -128,11 +128,14 @@ def _golden(golden_dir, name):
     ('power_train_b256', syn.POWER, True),
     ('power_exact_train_b64', syn.POWER_EXACT, True),
     ('toy_eval_b64', syn.TOY, False),
+    ('celebahq256_b1', syn.CELEBAHQ256, False),          # BASELINE.json configs[4]: 4 scales, 5 bits, 256 x 256
 ])
 def test_flow_matches_reference_golden(golden_dir, name, arch, train):
+    """Per block: Broyden nstep / lowest_step and the series length exact.  bits/dim or nats <= 1e-5; per-sample
+    log p <= 2e-3 nats + 2 fp32 ulps (|log p| reaches 2e4 nats at 3x32x32, 1e6 at 3x256x256); z <= 2e-4."""
     g = _golden(golden_dir, name)
     x = torch.from_numpy(g['x']).to(DEV)
-    m, _ = _model(arch, x.shape[0])
+    m, _ = _model(arch, x.shape[0], int(g['power_iters']) if 'power_iters' in g else 30)
     m.train(train)
     np.random.seed(int(g['seed']))
     torch.manual_seed(int(g['seed']))
@@ -145,10 +148,12 @@ def test_flow_matches_reference_golden(golden_dir, name, arch, train):
     blocks = imblocks(m)
     for i, b in enumerate(blocks):
         assert b.last_broyden['nstep'] == int(g['b%d_nstep' % i]), 'block %d nstep' % i
+        if 'b%d_lowest_step' % i in g and b.last_broyden['nstep'] > 0:
+            assert b.last_broyden['lowest_step'] == int(g['b%d_lowest_step' % i]), 'block %d lowest_step' % i
         if 'b%d_n_power_series' % i in g:
             assert b.last_n_power_series == int(g['b%d_n_power_series' % i][0])
     assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
-    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(logpx.view(-1).cpu().numpy(), g['logpx'], rtol=4e-7, atol=2e-3)
     np.testing.assert_allclose(z.reshape(z.shape[0], -1).cpu().numpy(), g['z'], rtol=0, atol=2e-4)
 
 
@@ -516,17 +521,15 @@ def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
         _close(a, b, rel=1e-5)
 
 
-@pytest.mark.parametrize('d1rc', [1, 0])
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3])
-def test_fused_k128_vjp_matches_64px_kernel(block, B, d1rc):
+def test_fused_k128_vjp_matches_64px_kernel(block, B):
     """The 128-pixel K-chunked kernel (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
     256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net forward, the VJP, the chained log-det
     series (each term stages the previous term's taps, preact swish' and trace partial) and the Neumann vector
     (each term stages the accumulation w += c_k v_k), with the workspace and every CU's LDS NaN-poisoned before
-    each call.  INF_OPT_FUSED_K128 = 2 forces the 128-pixel kernel at these small grids; INF_OPT_D1_RECOMPUTE selects
-    whether it recomputes its epilogue multiplier d1 from the primal input (1) or reads the saved one (0).  Tolerance:
-    1e-5 of max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons."""
+    each call.  INF_OPT_FUSED_K128 = 2 forces the 128-pixel kernel at these small grids.  Tolerance: 1e-5 of
+    max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons."""
     arch = syn.CIFAR10
     m, _ = _model(arch, B)
     blk = imblocks(m)[block]
@@ -549,7 +552,6 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, d1rc):
         ws.fill_(255)
         _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
     outs = {}
-    d_prev = net.set_option(_hip.INF_OPT_D1_RECOMPUTE, d1rc)
     k_prev = net.get_option(_hip.INF_OPT_FUSED_K128)
     try:
         for pol in (2, 0):
@@ -572,7 +574,6 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, d1rc):
             outs[pol] = (y, g, ld, w)
     finally:
         net.set_option(_hip.INF_OPT_FUSED_K128, k_prev)
-        net.set_option(_hip.INF_OPT_D1_RECOMPUTE, d_prev)
     assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_K128, 3) < 0
     assert net.get_option(_hip.INF_OPT_FUSED_K128) == k_prev
     for a in outs[2]:

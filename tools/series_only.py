@@ -20,7 +20,6 @@ ap.add_argument('--batch', type=int, default=64)
 ap.add_argument('--mfma', type=int, default=1)
 ap.add_argument('--reps', type=int, default=3)
 ap.add_argument('--terms', type=int, default=20)
-ap.add_argument('--d1rc', type=int, default=1, help='INF_OPT_D1_RECOMPUTE')
 ap.add_argument('--k128', type=int, default=1, help='INF_OPT_FUSED_K128')
 ap.add_argument('--single', type=int, default=0, help='one net (inf_logdet_series) instead of the pair')
 a = ap.parse_args()
@@ -42,7 +41,6 @@ nz = _hip.native_net(blk.nnet_z, x.shape[1:], x.device)
 for n_ in (nx, nz):
     n_.refresh_if_needed(st)
     _hip.check(n_.lib.inf_net_set_mfma(n_.handle, a.mfma), 'set')
-    n_.set_option(_hip.INF_OPT_D1_RECOMPUTE, a.d1rc)
     n_.set_option(_hip.INF_OPT_FUSED_K128, a.k128)
 ws = torch.empty(2 * max(nx.ws_bytes(B), nz.ws_bytes(B)), dtype=torch.uint8, device='cuda')
 out = torch.empty(2, B, device='cuda')
@@ -63,5 +61,5 @@ for r in range(a.reps + 1):
 t1.record()
 torch.cuda.synchronize()
 us = t0.elapsed_time(t1) / a.reps / a.terms * 1e3
-print('scale %d B %d mfma %d d1rc %d k128 %d %s: %.1f us/term, %.3f us/term/image' % (
-    a.scale, B, a.mfma, a.d1rc, a.k128, 'single' if a.single else 'pair', us, us / B / (1 if a.single else 2)))
+print('scale %d B %d mfma %d k128 %d %s: %.1f us/term, %.3f us/term/image' % (
+    a.scale, B, a.mfma, a.k128, 'single' if a.single else 'pair', us, us / B / (1 if a.single else 2)))
