@@ -1,0 +1,60 @@
+"""Diagnostic variants of the 128-pixel VJP kernel (fused313k.hip) for time attribution -- WRONG RESULTS, never
+shipped: the product source stays untouched; a patched copy is compiled into gpurun_alt/lib_<name>.so.
+
+    python tools/build_alt_k128.py <name> <variant>[,<variant>...]
+      d2l2   d2 read from image 0 / tile 0 for every tile (L2-resident: the HBM burst removed, the loads kept)
+      d1l2   the same for d1
+      nod2   no d2 loads at all (multiplier 1)
+      nod1   no d1 loads at all (multiplier 1)
+Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py, INFLOW_FUSED_TIMING=1 for the phase stamps).
+"""
+import os
+import subprocess
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+C = os.path.join(R, 'implicit-normalizing-flows_amd', 'csrc')
+O = os.path.join(R, 'implicit-normalizing-flows_amd', 'lib', '_hip', 'obj')
+
+
+def patch(src, variants):
+    rep = []
+    if 'd2l2' in variants:
+        rep.append(('const f32x4* q = dptr(a.d2, 8 * c + wid, b);',
+                    'const f32x4* q = reinterpret_cast<const f32x4*>(a.d2 + (((0 + (b >> 1)) * 16 + 8 * c + wid) * 2 + (b & 1)) * 1024 + lane * 16);'))
+    if 'd1l2' in variants:
+        rep.append(('const f32x4* q = dptr(a.d1, 2 * wid + m, b);',
+                    'const f32x4* q = reinterpret_cast<const f32x4*>(a.d1 + (((0 + (b >> 1)) * 16 + 2 * wid + m) * 2 + (b & 1)) * 1024 + lane * 16);'))
+    if 'nod2' in variants:
+        rep.append(('for (int j = 0; j < 4; ++j) d2v[b][j] = q[j];',
+                    'for (int j = 0; j < 4; ++j) d2v[b][j] = f32x4{1.f, 1.f, 1.f, 1.f}; (void)q;'))
+    if 'nod1' in variants:
+        rep.append(('for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];',
+                    'for (int j = 0; j < 4; ++j) d1v[b][j] = f32x4{1.f, 1.f, 1.f, 1.f}; (void)q;'))
+    for old, new in rep:
+        assert src.count(old) == 1, old
+        src = src.replace(old, new)
+    return src
+
+
+def main():
+    name, variants = sys.argv[1], sys.argv[2].split(',')
+    src = patch(open(os.path.join(C, 'fused313k.hip')).read(), variants)
+    tmp = os.path.join(C, '_alt_%s.hip' % name)
+    with open(tmp, 'w') as f:
+        f.write(src)
+    os.makedirs(os.path.join(R, 'gpurun_alt'), exist_ok=True)
+    obj = '/tmp/alt_%s.o' % name
+    try:
+        subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC',
+                        '-ffp-contract=fast', '-c', '-o', obj, tmp], check=True)
+    finally:
+        os.remove(tmp)
+    objs = [os.path.join(O, f) for f in sorted(os.listdir(O)) if f.endswith('.o') and f != 'fused313k.o']
+    out = os.path.join(R, 'gpurun_alt', 'lib_%s.so' % name)
+    subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-shared', '-fPIC', '-o', out, obj] + objs, check=True)
+    print('built', out)
+
+
+if __name__ == '__main__':
+    main()
