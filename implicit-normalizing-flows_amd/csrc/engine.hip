@@ -1488,6 +1488,9 @@ int series_fused(InfNet* const* nets, const float* const* xs, const float* const
       Net313Args& v = args[i];
       v = net313_args(n, es[i], B, bf, true);
       v.Y = (k % 2 == 0) ? bf.Y : bf.Y2;
+      // serpentine: odd terms walk the tiles backwards, so a term starts on the derivative tiles the previous
+      // one read last (still in the memory-side cache: s0 pair 349 -> 338 us per term)
+      v.tile_order = k & 1;
       if (k > 0) {
         v.in = nullptr;
         v.in_taps = (k % 2 == 1) ? bf.Y : bf.Y2;

@@ -1160,6 +1160,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     return e ? atoi(e) : 0;
   }();
   pr.dbg = dbg;
+  pr.reverse = a0.tile_order;
   static const bool timing = getenv("INFLOW_FUSED_TIMING") != nullptr;
   pr.tbuf = nullptr;
   if (timing) pr.tbuf = timing_buf(pr.nb0 * nnets);

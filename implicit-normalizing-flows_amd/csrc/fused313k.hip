@@ -74,9 +74,10 @@ int net313k_fits(int hid, int C, int H, int W) {
 template <int MODE>
 __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   constexpr bool VJP = MODE == MODE_VJP;
-  const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
+  const int bx = pr.reverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int sel = bx >= pr.nb0 ? 1 : 0;
   const Net313Args& a = pr.a[sel];
-  const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
+  const int bid = bx - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[KB_LDS];
 #define KSTAMP(i_)                                                                             \
   do {                                                                                         \
@@ -110,7 +111,9 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   };
   // phase A's multiplier d2 for one chunk (this wave's 32 rows x 128 pixels), requested ahead of its use: chunk 0's
   // before the staging; chunk 1's first two column blocks right after phase B of chunk 0 (the registers beside
-  // the phase-B accumulators allow 32), its last two at the start of phase A
+  // the phase-B accumulators allow 32), its last two at the start of phase A.  (A wave's vector loads complete
+  // in order, so a later load waits for the d2 burst wherever it is placed: requested after the staging barrier
+  // instead, the staging got 6k cycles shorter and phase A as much longer.)
   f32x4 d2v[KB_NB][4];
   auto loadD2 = [&](int c, int b0, int b1) {
 #pragma unroll

@@ -180,6 +180,7 @@ struct Net313Args {
   float acc_coef;         //   implicit_block.py:430-436), v the previous term's VJP after the tap sum
   int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
                           //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
+  int tile_order;         // 1: the 128-pixel kernel walks the tiles backwards (series terms alternate; args[0])
 };
 struct Net313Pair {
   Net313Args a[2];
@@ -188,6 +189,7 @@ struct Net313Pair {
   unsigned long long* tbuf;   // INFLOW_FUSED_TIMING: per-workgroup s_memtime stamps at phase boundaries
   int dbg;                // timing-attribution knob (INFLOW_FUSED_DBG, wrong results when set): 1 skip the
                           // d1 load, 2 skip the d2 load, 4 skip phase C, 8 skip the input staging
+  int reverse;            // 128-pixel kernel: workgroup i runs tile nb - 1 - i (alternating series terms)
 };
 int net313_supported(int hid, int C, int H, int W);
 // 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
