@@ -102,6 +102,8 @@ struct InfNet {
   // exponents per direction: Fexp[3 * vjp + phase]
   uint16_t* Fh[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int* Fexp = nullptr;
+  // Fh[4], Fh[5] (phase C, forward / VJP) with the k index's bits 2 and 3 swapped per 16-k tile (launch_permute_k23)
+  uint16_t* Fhp[2] = {nullptr, nullptr};
   int mfma_mode = INF_MFMA_F32;                 // InfMfmaMode of the fused kernel's phase B
   // f(0) of a conv net (the same image for every sample: zero input, zero padding), cached for the first
   // Broyden residual; computed by a launch of the same batch size (same tile variant -> same bits)
@@ -252,6 +254,7 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.A2h = h3 ? (const void*)n->Fh[vjp ? 3 : 2] : nullptr;
   f.A3h = h3 ? (const void*)n->Fh[vjp ? 5 : 4] : nullptr;
   f.Ah_exp = h3 ? n->Fexp + (vjp ? 3 : 0) : nullptr;
+  f.A3p = h3 ? (const void*)n->Fhp[vjp ? 1 : 0] : nullptr;
   f.M3 = n->M3;
   f.M3pad = n->M3pad;
   f.b1 = n->L[0].b;
@@ -1209,6 +1212,7 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       floats += 3 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64;
       // F16X3 planes: 2 fp16 (= 1 float) per element of each of the six operands, plus the scale exponents
       floats += 2 * ((size_t)n->fhid * n->K1pad + (size_t)n->fhid * n->fhid + (size_t)n->M3pad * n->fhid) + 6 * 64 + 64;
+      floats += 2 * (size_t)n->M3pad * n->fhid + 2 * 64;   // the permuted phase-C planes Fhp
       n->rows_max = std::max(n->rows_max, n->M3);
       const char* mm = getenv("INFLOW_MFMA");             // "f32" / "fp32" / "bf16x6" / "f16x3" (default)
       n->mfma_mode = INF_MFMA_F16X3;
@@ -1269,6 +1273,10 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     }
     n->Fexp = reinterpret_cast<int*>(p);
     p += 64;
+    for (int i = 0; i < 2; ++i) {
+      n->Fhp[i] = reinterpret_cast<uint16_t*>(p);
+      p += (size_t)n->M3pad * n->fhid + 64;
+    }
   }
   *out = n;
   return INF_OK;
@@ -1315,6 +1323,7 @@ int inf_net_refresh(InfNet* n, void* stream) {
                          (long)n->M3pad * H};
     for (int i = 0; i < 6; ++i) INF_TRY(launch_split3(src[i], n->Fs[i], cnt[i], s));
     for (int i = 0; i < 6; ++i) INF_TRY(launch_split2h(src[i], n->Fh[i], cnt[i], n->Fexp + 3 * (i & 1) + i / 2, s));
+    for (int i = 0; i < 2; ++i) INF_TRY(launch_permute_k23(n->Fh[4 + i], n->Fhp[i], cnt[4 + i] / 512, s));
   }
   return INF_OK;
 }

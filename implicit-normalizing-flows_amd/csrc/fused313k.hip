@@ -5,24 +5,36 @@
 // pipe.  Twice the pixels per workgroup halves the weight bytes per pixel, but a 512 x 128 fp32
 // activation tile (256 KiB) does not fit the 160 KiB LDS.  So the HID dimension is cut into two 256-row
 // chunks, and each chunk of an activation goes through LDS once, already split into the fp16 (h, l)
-// planes phase B / C consume (128 KiB per chunk):
+// planes phase B consumes (128 KiB per chunk):
 //
 //   stage halo (series chaining as in fused313.hip)
 //   for chunk c in {0, 1}:
 //     phase A rows [256c, 256c + 256): t = (W_A^T-flipped . im2col(v)) * d2        (per wave 32 rows)
 //     per-column scale over the chunk, split -> LDS chunk buffer                    (2 barriers)
 //     phase B, K = the chunk's 256 rows: acc += W_B^T[:, chunk] . t_chunk            (per wave 64 x 128)
-//   t2 = acc * d1; per-column scale over all 512 rows
-//   for chunk c in {0, 1}: waves holding rows of c split them -> LDS; phase C over the chunk's K tiles
-//   (split-K partials reduced through LDS) -> packed taps Y
+//   t2 = acc * d1 (this wave's 64 rows), per-column scale over those rows, split in registers
+//   phase C from registers: per 32-row block of the 9C taps, each wave contracts its own 64 rows of t2
+//   (K = 64) into a partial; the 8 partials are summed in a fixed order through LDS -> packed taps Y
 //
 // The phase-B B operand is two ds_read_b128 per 32-pixel column and K tile (no split VALU in the loop),
 // and each weight fragment feeds 4 column blocks (24 MFMAs per 4 KiB of weight loads per wave).
 // Chunk scales: each chunk has its own power-of-two column scale; the phase-B accumulator is moved to the
 // second chunk's scale by an exact ldexp between the chunks (the two exponents are kept within 60 of
 // each other, so no finite partial sum over- or underflows).
+//
+// Phase C needs no LDS operand: the phase-B accumulator of lane (n, lh) holds rows 8j + 4lh + q (j, q = 0..3) of
+// column n, and a 32x32x16 B operand wants 8 k-slots 8lh + s of column n per lane.  Slot s = 4a + q of K tile t
+// takes row 16t + 8a + 4lh + q, i.e. the k index with bits 2 and 3 swapped; the phase-C weights are packed with the
+// same swap (A3p, launch_permute_k23), so the contraction is unchanged.  Each wave scales its partial on its own
+// column maxima (no barrier) and unscales it exactly before the sum.  Against the LDS-operand version this removes
+// two chunk puts and their barriers and cuts the phase-C weight stream 4x (each wave reads the weights of its own
+// 64 rows once instead of every column block reading all 512).
+//
 // d1 / d2 are read in the 64-pixel kernel's fragment layout (the SAVE launches of the pair write them):
 // 128-pixel tile t covers 64-pixel tiles 2t, 2t + 1.
+//
+// The geometry (C, W) of the CIFAR scales is a template parameter (CT, WT; 0 = from the arguments), so the halo
+// index arithmetic, phase A's K loop and phase C's row-block loop are compile-time.
 #include <type_traits>
 
 #include "kernels.h"
@@ -55,6 +67,8 @@ __device__ __forceinline__ void split4h(float v0, float v1, float v2, float v3, 
   h = make_uint2(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b));
   l = make_uint2(__builtin_bit_cast(unsigned, c), __builtin_bit_cast(unsigned, d));
 }
+
+constexpr int kb_seg(int W) { return W < KB_BN ? W : KB_BN; }
 }  // namespace
 
 // 128-pixel tiles fit: whole image rows (or a 128-wide row segment), halo + im2col table + chunk buffer
@@ -63,7 +77,7 @@ int net313k_fits(int hid, int C, int H, int W) {
   const int P = H * W;
   const int seg = W < KB_BN ? W : KB_BN;
   if (P % KB_BN != 0 || KB_BN % seg != 0 || (W > KB_BN && W % KB_BN != 0)) return 0;
-  if (9 * C > 256) return 0;                      // phase C: at most 8 row blocks x 4 columns = 4 jobs per wave
+  if (9 * C > 256) return 0;                      // phase A: at most 16 K tiles
   const int rows = KB_BN / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
   const long need = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
@@ -71,7 +85,7 @@ int net313k_fits(int hid, int C, int H, int W) {
 }
 
 // MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2))
-template <int MODE>
+template <int MODE, int CT, int WT>
 __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   constexpr bool VJP = MODE == MODE_VJP;
   const int bx = pr.reverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
@@ -83,18 +97,34 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   do {                                                                                         \
     if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+  // stamps 8..15 inside chunk 1 and phase C (INFLOW_FUSED_TIMING), fenced with sched_barrier: the fences stay in every
+  // build, they keep the compiler from hoisting the next phase's loads into the current one (measured faster with
+  // them: 308 vs 321 us per s0 series term, 110 vs 114 at s1)
+#define KSUB(i_)                                                                               \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + (i_)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+  } while (0)
   KSTAMP(0);
   if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  const int P = a.H * a.W;
+  // geometry: compile-time for the instantiated scales
+  const int C = CT ? CT : a.C;
+  const int W = WT ? WT : a.W;
+  const int seg = WT ? kb_seg(WT) : a.seg;
+  const int rows = KB_BN / seg;
+  const int K1pad = CT ? (9 * CT + 15) / 16 * 16 : a.K1pad;
+  const int M3 = 9 * C;
+  const int nrb = CT ? (9 * CT + 31) / 32 : a.M3pad / 32;
+  const int P = a.H * W;
   const int tiles_per_img = P / KB_BN;
   const int img = bid / tiles_per_img, tile = bid - img * tiles_per_img;
   const int p0 = tile * KB_BN;
-  const int seg = a.seg, rows = KB_BN / seg;
-  const int y0 = p0 / a.W, x0 = p0 - y0 * a.W;
+  const int y0 = p0 / W, x0 = p0 - y0 * W;
   const int RH = rows + 2, CW = seg + 2;
-  const int vhn = a.C * RH * CW;
+  const int vhn = C * RH * CW;
   const int vhz = vhn + rows * CW;                  // zero run for the K-padding rows of phase A
   // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] | trace partials [NW] (fp64) | koff | halo
   u32x4* cb = reinterpret_cast<u32x4*>(smem);
@@ -102,7 +132,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   float* hmax = cmax + KB_NW * KB_BN;
   double* red = reinterpret_cast<double*>(hmax + 8);
   int* koff = reinterpret_cast<int*>(red + KB_NW);
-  float* vh = reinterpret_cast<float*>(koff + a.K1pad);
+  float* vh = reinterpret_cast<float*>(koff + K1pad);
 
   // d1 / d2 in the 64-pixel kernel's fragment order: 64-px tile (2 tile + b / 2), column (b & 1), row block rb
   const long tile64 = (long)img * (P / 64) + 2 * tile;
@@ -130,15 +160,15 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   float hmx = 0.f;
   double dacc = 0.0;
   {
-    const float* in = a.in ? a.in + (long)img * a.C * P : nullptr;
+    const float* in = a.in ? a.in + (long)img * C * P : nullptr;
     if (a.in_taps) {
-      const float* ytap = a.in_taps + (long)img * a.M3 * P;
-      const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
-      const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
+      const float* ytap = a.in_taps + (long)img * M3 * P;
+      const float* mx = a.vmul_x ? a.vmul_x + (long)img * C * P : nullptr;
+      const float* ep = a.dot_eps ? a.dot_eps + (long)img * C * P : nullptr;
       const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
       const float* mxp = mx ? mx : ytap;
       const float* epp = ep ? ep : ytap;
-      float* accw = a.acc_w ? a.acc_w + (long)img * a.C * P : nullptr;
+      float* accw = a.acc_w ? a.acc_w + (long)img * C * P : nullptr;
       const float* awp = accw ? accw : ytap;
       auto pass = [&](auto nuc, int i0) {
         constexpr int NU = decltype(nuc)::value;
@@ -149,13 +179,13 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           const int ic = i < vhn ? i : 0;
           const int c = ic / (RH * CW), rr = ic - c * RH * CW;
           const int hy = rr / CW, hx = rr - hy * CW;
-          const int yq = min(max(y0 + hy - 1, 0), a.H - 1), xq = min(max(x0 + hx - 1, 0), a.W - 1);
-          const long ee = (long)c * P + yq * a.W + xq;
+          const int yq = min(max(y0 + hy - 1, 0), a.H - 1), xq = min(max(x0 + hx - 1, 0), W - 1);
+          const long ee = (long)c * P + yq * W + xq;
           const float* yc = ytap + (long)c * 9 * P;
 #pragma unroll
           for (int tp = 0; tp < 9; ++tp) {
-            const int y2 = min(max(yq + tp / 3 - 1, 0), a.H - 1), x2 = min(max(xq + tp % 3 - 1, 0), a.W - 1);
-            tv[u][tp] = yc[(long)tp * P + y2 * a.W + x2];
+            const int y2 = min(max(yq + tp / 3 - 1, 0), a.H - 1), x2 = min(max(xq + tp % 3 - 1, 0), W - 1);
+            tv[u][tp] = yc[(long)tp * P + y2 * W + x2];
           }
           xm[u] = mxp[ee];
           ev[u] = epp[ee];
@@ -165,22 +195,22 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
         for (int u = 0; u < NU; ++u) {
           const int i = i0 + u * KB_NT;
           const int ic = i < vhn ? i : 0;
-          const int rr = ic % (RH * CW);
+          const int c = ic / (RH * CW), rr = ic - c * RH * CW;
           const int hy = rr / CW, hx = rr - hy * CW;
           const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-          const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+          const bool in_img = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < W;
           const int ok = in_img ? ((hy >= 1 && hy <= rows && hx >= 1 && hx <= seg) ? 2 : 1) : 0;
           float v = 0.f;
 #pragma unroll
           for (int tp = 0; tp < 9; ++tp) {
             const int y2 = yy + tp / 3 - 1, x2 = xx + tp % 3 - 1;
-            const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W;
+            const bool vt = y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < W;
             v += vt ? tv[u][tp] : 0.f;
           }
           if (mx) v = v * swish_fast_d(xm[u], msp);
           v = ok ? v : 0.f;
           if (ep && ok == 2) dacc += (double)v * (double)ev[u];
-          if (accw && ok == 2) accw[(long)(ic / (RH * CW)) * P + yy * a.W + xx] = fmaf(a.acc_coef, v, wv[u]);
+          if (accw && ok == 2) accw[(long)c * P + yy * W + xx] = fmaf(a.acc_coef, v, wv[u]);
           hmx = fmaxf(hmx, fabsf(v));
           if (i < vhz) vh[i] = v;
         }
@@ -201,8 +231,8 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           const int c = i / (RH * CW), rr = i - c * RH * CW;
           const int hy = rr / CW, hx = rr - hy * CW;
           const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-          if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-            v = in[(long)c * P + yy * a.W + xx];
+          if (yy >= 0 && yy < a.H && xx >= 0 && xx < W) {
+            v = in[(long)c * P + yy * W + xx];
             if (a.pre_beta) v = swish_fast_f(v, pre_sp);
           }
         }
@@ -219,9 +249,9 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     const double w = wave_sum(dacc);
     if (lane == 0) red[wid] = w;
   }
-  for (int k = tid; k < a.K1pad; k += KB_NT) {
+  for (int k = tid; k < K1pad; k += KB_NT) {
     int o = vhn;                                    // zero run for the K padding
-    if (k < 9 * a.C) {
+    if (k < 9 * C) {
       const int c = k / 9, tt = k - c * 9;
       o = c * RH * CW + (tt / 3) * CW + (tt % 3);
     }
@@ -255,8 +285,8 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   }
   const u32x4* A1h = reinterpret_cast<const u32x4*>(a.A1h);
   const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);
-  const u32x4* A3h = reinterpret_cast<const u32x4*>(a.A3h);
-  const int nkt1 = a.K1pad / 16;
+  const u32x4* A3p = reinterpret_cast<const u32x4*>(a.A3p);
+  const int nkt1 = K1pad / 16;
   const int ew = a.Ah_exp[1];
   const float sp1 = VJP ? 0.f : softplus_f(*a.beta1), sp2 = VJP ? 0.f : softplus_f(*a.beta2);
 
@@ -286,6 +316,13 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
   for (int b = 0; b < KB_NB; ++b) scB[b] = 0;
 
+  // chunk 1's phase-A weights, requested at the end of phase B of chunk 0 ahead of chunk 1's d2 (a wave's loads
+  // complete in order): with a short K loop (compile-time, <= 4 K tiles) they stay in registers for the four
+  // column-block passes
+  constexpr int NKT1 = CT ? (9 * CT + 15) / 16 : 0;
+  constexpr bool PRE_A1 = NKT1 > 0 && NKT1 <= 4;
+  u32x4 wA1[PRE_A1 ? NKT1 : 1][2];
+
   // the two chunks as separate code (chunk 0 starts from known-zero accumulators)
   auto chunk = [&](auto cc) {
     constexpr int c = decltype(cc)::value;
@@ -302,7 +339,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) ac[g][r] = 0.f;
       u32x4 w0[2], w1[2];
-      ldw2(A1h, (long)rbA * nkt1, lane, w0);
+      if (!(PRE_A1 && c == 1)) ldw2(A1h, (long)rbA * nkt1, lane, w0);
       auto stepA = [&](int kt, const u32x4 (&af)[2]) {
         const int* kp = koff + kt * 16 + lh * 8;
         const int4 k0 = *reinterpret_cast<const int4*>(kp);
@@ -318,12 +355,17 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           ac[g] = mfma_h3(af, h, l, ac[g]);
         }
       };
-      for (int kt = 0; kt < nkt1; kt += 2) {
-        const bool has1 = kt + 1 < nkt1;
-        if (has1) ldw2(A1h, (long)rbA * nkt1 + kt + 1, lane, w1);
-        stepA(kt, w0);
-        if (kt + 2 < nkt1) ldw2(A1h, (long)rbA * nkt1 + kt + 2, lane, w0);
-        if (has1) stepA(kt + 1, w1);
+      if constexpr (PRE_A1 && c == 1) {
+#pragma unroll
+        for (int kt = 0; kt < NKT1; ++kt) stepA(kt, wA1[kt]);
+      } else {
+        for (int kt = 0; kt < nkt1; kt += 2) {
+          const bool has1 = kt + 1 < nkt1;
+          if (has1) ldw2(A1h, (long)rbA * nkt1 + kt + 1, lane, w1);
+          stepA(kt, w0);
+          if (kt + 2 < nkt1) ldw2(A1h, (long)rbA * nkt1 + kt + 2, lane, w0);
+          if (has1) stepA(kt + 1, w1);
+        }
       }
       // epilogue A: unscale, times d2 = swish'(a2) (the VJP through the second activation)
 #pragma unroll
@@ -358,12 +400,15 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       phaseA(std::integral_constant<int, KB_NB>(), std::integral_constant<int, 0>());
     } else {
       phaseA(I1(), std::integral_constant<int, 0>());
+      KSUB(1);
       phaseA(I1(), std::integral_constant<int, 1>());
       phaseA(I1(), std::integral_constant<int, 2>());
       phaseA(I1(), std::integral_constant<int, 3>());
+      KSUB(2);
     }
     __syncthreads();      // column maxima visible; every wave is done reading the previous chunk buffer
     if (c == 0) KSTAMP(2);
+    if (c == 1) KSUB(3);
     // chunk column scales; chunk 1 stays within 2^60 of chunk 0 and the accumulator moves to its scale
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
@@ -384,6 +429,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     }
     __syncthreads();      // chunk buffer complete
     if (c == 0) KSTAMP(3);
+    if (c == 1) KSUB(4);
     // ------------------------------------------------ phase B over the chunk's 16 K tiles
     {
       const int rbw = 2 * wid;
@@ -420,16 +466,20 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     }
     if constexpr (c == 0) {
       KSTAMP(4);
+      KSUB(0);
+      if constexpr (PRE_A1) {
+#pragma unroll
+        for (int kt = 0; kt < NKT1; ++kt) ldw2(A1h, (long)(8 + wid) * NKT1 + kt, lane, wA1[kt]);
+      }
       loadD2(1, 0, 2);
     }
   };
   chunk(std::integral_constant<int, 0>());
   chunk(std::integral_constant<int, 1>());
   KSTAMP(5);
+  KSUB(5);
+
   // ------------------------------------------------ epilogue B: unscale, times d1 = swish'(a1)
-  float cmC[KB_NB];
-#pragma unroll
-  for (int b = 0; b < KB_NB; ++b) cmC[b] = 0.f;
   // (one row block at a time: its 4 column blocks' d1 requested together, 64 registers)
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
@@ -449,7 +499,6 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
         for (int r = 0; r < 16; ++r) {
           const int row = (2 * wid + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           acc[m][b][r] = swish_fast_f(__builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row], sp2);
-          cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
         }
         continue;
       }
@@ -461,127 +510,104 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
         acc[m][b][4 * j + 2] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j + 2], e) * d.z;
         acc[m][b][4 * j + 3] = __builtin_amdgcn_ldexpf(acc[m][b][4 * j + 3], e) * d.w;
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) cmC[b] = fmaxf(cmC[b], fabsf(acc[m][b][r]));
     }
+    if (m == 0) KSUB(6);
   }
+  // ------------------------------------------------ phase C from registers
+  // column scale over this wave's 64 rows; t2 split in place into the B operands of its 4 K tiles
+  // (K tile kk = 2 m + t of the wave = global K tile 4 wid + kk; slot s = 4a + q <- acc[m][b][8t + s])
+  int sw[KB_NB];
 #pragma unroll
   for (int b = 0; b < KB_NB; ++b) {
-    const float cm = fmaxf(cmC[b], __shfl_xor(cmC[b], 32, 64));
-    if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;   // (free: every wave read it before the last barrier)
+    float cm = 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(acc[m][b][r]));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    sw[b] = h3_scale_exp(cm);
   }
-  __syncthreads();        // column maxima of t2 visible; every wave is done with the phase-B chunk buffer
-  float sC[KB_NB];
+  u32x4 bh[4][KB_NB], bl[4][KB_NB];
+#pragma unroll
+  for (int b = 0; b < KB_NB; ++b) {
+    const float S = __builtin_amdgcn_ldexpf(1.f, sw[b]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      float x[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) x[s] = acc[kk >> 1][b][8 * (kk & 1) + s];
+      split2h(x, S, bh[kk][b], bl[kk][b]);
+    }
+  }
+  const int ew3 = a.Ah_exp[2];
   int eC[KB_NB];
 #pragma unroll
-  for (int b = 0; b < KB_NB; ++b) {
-    float m_ = 0.f;
+  for (int b = 0; b < KB_NB; ++b) eC[b] = -(sw[b] + ew3);
+  KSTAMP(6);
+  float* Y = a.Y + (long)img * M3 * P;
+  float* part = smem;                                // [wave][column block][16][64]: the chunk buffer's space
+  // the four weight fragments of the first row block, in flight across the barrier
+  u32x4 w3[4][2];
 #pragma unroll
-    for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, cmax[w * KB_BN + b * 32 + li]);
-    const int sc = h3_scale_exp(m_);
-    sC[b] = __builtin_amdgcn_ldexpf(1.f, sc);
-    eC[b] = -(sc + a.Ah_exp[2]);
-  }
-  // ------------------------------------------------ phase C: jobs = (row block of the 9C taps) x column block
-  const int nrb = a.M3pad / 32;
-  const int ntask = nrb * KB_NB;
-  int ksplit = 1;
-  while (ntask * ksplit * 2 <= KB_NW) ksplit *= 2;
-  const int kts = 16 / ksplit;                       // K tiles per job and chunk
-  const int njobs = ntask * ksplit;                  // <= 32 (net313k_fits)
-  f32x16 cacc[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cacc[jj][r] = 0.f;
-  // with ksplit == 1 a wave's jobs (wid + 8 jj) share the column block wid % 4; with ksplit > 1 one job each
-  const int job0 = wid;
-  const int ks = job0 % ksplit;
-  const int bC = (job0 / ksplit) % KB_NB;
+  for (int kk = 0; kk < 4; ++kk) ldw2(A3p, 4 * wid + kk, lane, w3[kk]);
+  __syncthreads();                                   // every wave is done reading the phase-B chunk buffer
 #pragma unroll 1
-  for (int c = 0; c < 2; ++c) {
-    if (wid / 4 == c) {                                // this wave's t2 rows belong to chunk c
+  for (int rb = 0; rb < nrb; ++rb) {
+    f32x16 cacc[KB_NB];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+    for (int b = 0; b < KB_NB; ++b)
 #pragma unroll
-        for (int b = 0; b < KB_NB; ++b) {
-          float v[16];
+      for (int r = 0; r < 16; ++r) cacc[b][r] = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = acc[m][b][r];
-          put(4 * (wid & 3) + 2 * m, b, v, sC[b]);
-        }
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int b = 0; b < KB_NB; ++b) cacc[b] = mfma_h3(w3[kk], bh[kk][b], bl[kk][b], cacc[b]);
+      if (rb + 1 < nrb) ldw2(A3p, (long)(rb + 1) * 32 + 4 * wid + kk, lane, w3[kk]);   // the next row block's
     }
+#pragma unroll
+    for (int b = 0; b < KB_NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) part[((wid * KB_NB + b) * 16 + r) * 64 + lane] = __builtin_amdgcn_ldexpf(cacc[b][r], eC[b]);
+    KSUB(7);
     __syncthreads();
-    if (c == 0) KSTAMP(6);
-    const int k_lo = ks * kts;
-    for (int jj = 0; jj < 4; ++jj) {
-      const int job = job0 + KB_NW * jj;
-      if (job >= njobs) break;
-      const int rb = (job / ksplit) / KB_NB;
-      u32x4 w0[2], w1[2];
-      ldw2(A3h, (long)rb * 32 + 16 * c + k_lo, lane, w0);
-      for (int kt = k_lo; kt < k_lo + kts; kt += 2) {
-        ldw2(A3h, (long)rb * 32 + 16 * c + kt + 1, lane, w1);
-        {
-          const u32x4 h = cb[((kt * KB_NB + bC) * 2) * 64 + lane], l = cb[((kt * KB_NB + bC) * 2 + 1) * 64 + lane];
-          cacc[jj] = mfma_h3(w0, h, l, cacc[jj]);
-        }
-        if (kt + 2 < k_lo + kts) ldw2(A3h, (long)rb * 32 + 16 * c + kt + 2, lane, w0);
-        {
-          const u32x4 h = cb[(((kt + 1) * KB_NB + bC) * 2) * 64 + lane], l = cb[(((kt + 1) * KB_NB + bC) * 2 + 1) * 64 + lane];
-          cacc[jj] = mfma_h3(w1, h, l, cacc[jj]);
-        }
-      }
-    }
-    if (c == 0) __syncthreads();                       // chunk 1's rows overwrite the buffer
-  }
-  KSTAMP(7);
-  float* Y = a.Y + (long)img * a.M3 * P;
-  const int n_out = bC * 32 + li, py_out = n_out / seg;
-  const int gcol = (y0 + py_out) * a.W + x0 + (n_out - py_out * seg);
-  int eCj = 0;                                       // unscale exponent of this wave's column block
+    // the 8 partials of each output in wave order; four outputs (b, r, lanes 4u .. 4u + 3) per thread and step: four
+    // consecutive pixels of one tap row (seg is a multiple of 4)
 #pragma unroll
-  for (int b = 0; b < KB_NB; ++b) eCj = b == bC ? eC[b] : eCj;
-  if (ksplit == 1) {
+    for (int i0 = 0; i0 < KB_NB * 256; i0 += KB_NT) {
+      const int i = i0 + tid;
+      const int b = i >> 8, r = (i >> 4) & 15, ln = (i & 15) * 4;
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int job = job0 + KB_NW * jj;
-      if (job >= njobs) break;
-      const int rb = job / KB_NB;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < a.M3) Y[(long)row * P + gcol] = __builtin_amdgcn_ldexpf(cacc[jj][r], eCj);
-      }
-    }
-  } else {
-    float* part = smem;                                // the chunk buffer is free after this barrier
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) part[(job0 * 16 + r) * 64 + lane] = __builtin_amdgcn_ldexpf(cacc[0][r], eCj);
-    __syncthreads();
-    for (int i = tid; i < ntask * 1024; i += KB_NT) {
-      const int task = i >> 10, rem = i & 1023, r = rem >> 6, ln = rem & 63;
-      float sum = 0.f;
-      for (int k = 0; k < ksplit; ++k) sum += part[((task * ksplit + k) * 16 + r) * 64 + ln];
-      const int rb = task / KB_NB, b = task % KB_NB;
+      for (int w = 0; w < KB_NW; ++w) sum += *reinterpret_cast<const f32x4*>(part + ((w * KB_NB + b) * 16 + r) * 64 + ln);
       const int row = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
       const int n = b * 32 + (ln & 31), py = n / seg;
-      if (row < a.M3) Y[(long)row * P + (y0 + py) * a.W + x0 + (n - py * seg)] = sum;
+      if (row < M3) *reinterpret_cast<f32x4*>(Y + (long)row * P + (y0 + py) * W + x0 + (n - py * seg)) = sum;
     }
+    if (rb + 1 < nrb) __syncthreads();               // the next row block's partials overwrite these
   }
+  KSTAMP(7);
   if (pr.tbuf && threadIdx.x == 0) {
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();
     pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
-    for (int v = 0; v < 16; ++v) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + v] = t_;
+    for (int v = 8; v < 16; ++v) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + v] = t_;
   }
+#undef KSUB
 #undef KSTAMP
 }
 
 int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s) {
-  if (mode == MODE_VJP) hipLaunchKernelGGL(net313k_kernel<MODE_VJP>, dim3(nb), dim3(KB_NT), 0, s, pr);
-  else if (mode == MODE_EVAL) hipLaunchKernelGGL(net313k_kernel<MODE_EVAL>, dim3(nb), dim3(KB_NT), 0, s, pr);
-  else return INF_ERR_UNSUPPORTED;
+  if (pr.a[0].A3p == nullptr || pr.a[1].A3p == nullptr) return INF_ERR_UNSUPPORTED;
+  const int C = pr.a[0].C, W = pr.a[0].W;
+#define K128_GEO(CT_, WT_)                                                                                        \
+  do {                                                                                                            \
+    if (mode == MODE_VJP) hipLaunchKernelGGL((net313k_kernel<MODE_VJP, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr); \
+    else hipLaunchKernelGGL((net313k_kernel<MODE_EVAL, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr);              \
+  } while (0)
+  if (mode != MODE_VJP && mode != MODE_EVAL) return INF_ERR_UNSUPPORTED;
+  if (C == 3 && W == 32) K128_GEO(3, 32);            // CIFAR-10 scale 0
+  else if (C == 12 && W == 16) K128_GEO(12, 16);     // CIFAR-10 scale 1
+  else K128_GEO(0, 0);
+#undef K128_GEO
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

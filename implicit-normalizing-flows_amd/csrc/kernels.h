@@ -121,6 +121,9 @@ int launch_split3(const float* src, uint16_t* dst, long n, hipStream_t s);
 // Scale exponent of a whole operand (*exp_out = h3_scale_exp(max |src|), common.h) and its two scaled fp16
 // planes per 512-float fragment tile: dst[(tile * 2 + plane) * 512 + w] (fused313.hip phase B, F16X3).
 int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStream_t s);
+// Copy of fragment-major fp16 planes (launch_split2h layout, ntiles fragment tiles of 2 x 512 halves) with the k index
+// of every 32x16 fragment tile permuted: slot (lane (i, h), 4a + q) <- slot (lane (i, a), 4h + q), i.e. k bits 2, 3 swapped
+int launch_permute_k23(const uint16_t* src, uint16_t* dst, long ntiles, hipStream_t s);
 
 // exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
@@ -159,6 +162,8 @@ struct Net313Args {
   const void* A2h;
   const void* A3h;
   const int* Ah_exp;
+  const void* A3p;        // A3h with the k index's bits 2 and 3 swapped inside every 16-k tile (launch_permute_k23):
+                          // phase C of the 128-pixel kernel takes its B operand straight from the phase-B accumulators
   int M3, M3pad;          // 9C taps rows
   const float* b1;
   const float* beta1;

@@ -782,6 +782,21 @@ int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStr
   return INF_OK;
 }
 
+__global__ void permute_k23_kernel(const uint16_t* src, uint16_t* dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long base = i & ~511L;                     // (tile, plane) block of 64 lanes x 8 halves
+  const int w = (int)(i & 511), L = w >> 3, s = w & 7;
+  const int li = L & 31, lh = L >> 5, a = s >> 2, q = s & 3;
+  dst[i] = src[base + (li + 32 * a) * 8 + 4 * lh + q];
+}
+int launch_permute_k23(const uint16_t* src, uint16_t* dst, long ntiles, hipStream_t s) {
+  const long n = ntiles * 1024;
+  hipLaunchKernelGGL(permute_k23_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // exact log|det(I + T)| per sample (torch.logdet via LU, implicit_block.py:253-258).  T is stored
 // feature-major as tangents: T[i][j] of sample b at tang[i * ld + (j + 1) * stride_j + b],

@@ -6,6 +6,7 @@ shipped: the product source stays untouched; a patched copy is compiled into gpu
       d1l2   the same for d1
       nod2   no d2 loads at all (multiplier 1)
       nod1   no d1 loads at all (multiplier 1)
+      sub    INFLOW_K128_SUBSTAMPS: stamps inside chunk 1 and phase C (results unchanged; sched_barrier fences)
 Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py, INFLOW_FUSED_TIMING=1 for the phase stamps).
 """
 import os
@@ -31,6 +32,8 @@ def patch(src, variants):
     if 'nod1' in variants:
         rep.append(('for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];',
                     'for (int j = 0; j < 4; ++j) d1v[b][j] = f32x4{1.f, 1.f, 1.f, 1.f}; (void)q;'))
+    if 'sub' in variants:
+        src = '#define INFLOW_K128_SUBSTAMPS 1\n' + src
     for old, new in rep:
         assert src.count(old) == 1, old
         src = src.replace(old, new)
