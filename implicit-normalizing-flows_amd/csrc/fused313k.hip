@@ -108,7 +108,8 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   } while (0)
   KSTAMP(0);
   if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // (the wave index through readfirstlane: wave-uniform, so the row-block addresses derived from it live in SGPRs)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, lh = lane >> 5;
   // geometry: compile-time for the instantiated scales
   const int C = CT ? CT : a.C;
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   };
   // phase A's multiplier d2 for one chunk (this wave's 32 rows x 128 pixels), requested ahead of its use: chunk 0's
   // before the staging; chunk 1's first two column blocks right after phase B of chunk 0 (the registers beside
-  // the phase-B accumulators allow 32), its last two at the start of phase A.  (A wave's vector loads complete
+  // the phase-B accumulators allow 32), the others one column-block pass ahead.  (A wave's vector loads complete
   // in order, so a later load waits for the d2 burst wherever it is placed: requested after the staging barrier
   // instead, the staging got 6k cycles shorter and phase A as much longer.)
   f32x4 d2v[KB_NB][4];
@@ -326,7 +327,6 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   // the two chunks as separate code (chunk 0 starts from known-zero accumulators)
   auto chunk = [&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if constexpr (c == 1) loadD2(1, 2, KB_NB);
     // ------------------------------------------------ phase A, rows of this wave in chunk c (row block 8c + wid)
     const int rbA = 8 * c + wid;
     float va[KB_NB][16];
@@ -392,6 +392,10 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
         for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
         cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
         if (lh == 0) cmax[wid * KB_BN + b * 32 + li] = cm;
+        if constexpr (c == 1) {                    // parked as fp32 in this wave's own part of the chunk buffer
+#pragma unroll
+          for (int r = 0; r < 16; ++r) smem[wid * 4096 + (b * 16 + r) * 64 + lane] = va[b][r];
+        }
       }
     };
     using I1 = std::integral_constant<int, 1>;
@@ -399,9 +403,16 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       // the phase-B accumulators are still zero constants: room for all four column blocks at once
       phaseA(std::integral_constant<int, KB_NB>(), std::integral_constant<int, 0>());
     } else {
+      // chunk 1: the phase-B accumulators hold 128 registers, so each column block's values are parked in LDS (in the
+      // 16 KiB of the chunk buffer this wave's put overwrites later) instead of registers; every wave must be done
+      // reading chunk 0's buffer first
+      __syncthreads();
+      // (d2 of column blocks 2 and 3 requested one pass ahead, in the registers of the blocks already used)
       phaseA(I1(), std::integral_constant<int, 0>());
       KSUB(1);
+      loadD2(1, 2, 3);
       phaseA(I1(), std::integral_constant<int, 1>());
+      loadD2(1, 3, 4);
       phaseA(I1(), std::integral_constant<int, 2>());
       phaseA(I1(), std::integral_constant<int, 3>());
       KSUB(2);
@@ -410,6 +421,12 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     if (c == 0) KSTAMP(2);
     if (c == 1) KSUB(3);
     // chunk column scales; chunk 1 stays within 2^60 of chunk 0 and the accumulator moves to its scale
+    if constexpr (c == 1) {                        // read back the parked values before the puts overwrite them
+#pragma unroll
+      for (int b = 0; b < KB_NB; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) va[b][r] = smem[wid * 4096 + (b * 16 + r) * 64 + lane];
+    }
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b) {
       float m_ = 0.f;
