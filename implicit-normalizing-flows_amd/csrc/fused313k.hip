@@ -155,7 +155,24 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       for (int j = 0; j < 4; ++j) d2v[b][j] = q[j];
     }
   };
-  loadD2(0, 0, KB_NB);
+  // phase A's weights (compile-time K loop of <= 4 tiles): chunk 0's requested with chunk 0's d2 after the staging
+  // loads, so phase A's MFMAs run while the d2 burst arrives (only its epilogue waits); chunk 1's (<= 4 tiles) at the
+  // end of phase B of chunk 0, ahead of chunk 1's d2
+  constexpr int NKT1 = CT ? (9 * CT + 15) / 16 : 0;
+  constexpr bool PRE_A0 = NKT1 > 0 && NKT1 <= 4;
+  constexpr bool PRE_A1 = NKT1 > 0 && NKT1 <= 4;
+  u32x4 wA0[PRE_A0 ? NKT1 : 1][2];
+  u32x4 wA1[PRE_A1 ? NKT1 : 1][2];
+  bool early_pending = true;                        // wave-uniform
+  auto issue_early = [&]() {
+    if constexpr (PRE_A0) {
+#pragma unroll
+      for (int kt = 0; kt < NKT1; ++kt) ldw2(reinterpret_cast<const u32x4*>(a.A1h), (long)wid * NKT1 + kt, lane, wA0[kt]);
+    }
+    loadD2(0, 0, KB_NB);
+    early_pending = false;
+  };
+  if (!PRE_A0 || !a.in_taps) issue_early();         // (without preloaded weights phase A would wait for d2 anyway)
 
   // ---- stage the input halo tile (series chaining: tap sum, preact swish', trace partial / Neumann acc) ----
   float hmx = 0.f;
@@ -192,6 +209,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           ev[u] = epp[ee];
           wv[u] = awp[ee];
         }
+        if (early_pending && i0 - tid + KB_NT * NU >= vhz) issue_early();   // after the last pass's loads
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           const int i = i0 + u * KB_NT;
@@ -317,12 +335,6 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
   for (int b = 0; b < KB_NB; ++b) scB[b] = 0;
 
-  // chunk 1's phase-A weights, requested at the end of phase B of chunk 0 ahead of chunk 1's d2 (a wave's loads
-  // complete in order): with a short K loop (compile-time, <= 4 K tiles) they stay in registers for the four
-  // column-block passes
-  constexpr int NKT1 = CT ? (9 * CT + 15) / 16 : 0;
-  constexpr bool PRE_A1 = NKT1 > 0 && NKT1 <= 4;
-  u32x4 wA1[PRE_A1 ? NKT1 : 1][2];
 
   // the two chunks as separate code (chunk 0 starts from known-zero accumulators)
   auto chunk = [&](auto cc) {
@@ -339,7 +351,8 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) ac[g][r] = 0.f;
       u32x4 w0[2], w1[2];
-      if (!(PRE_A1 && c == 1)) ldw2(A1h, (long)rbA * nkt1, lane, w0);
+      constexpr bool PRE = c == 0 ? PRE_A0 : PRE_A1;
+      if (!PRE) ldw2(A1h, (long)rbA * nkt1, lane, w0);
       auto stepA = [&](int kt, const u32x4 (&af)[2]) {
         const int* kp = koff + kt * 16 + lh * 8;
         const int4 k0 = *reinterpret_cast<const int4*>(kp);
@@ -355,7 +368,10 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           ac[g] = mfma_h3(af, h, l, ac[g]);
         }
       };
-      if constexpr (PRE_A1 && c == 1) {
+      if constexpr (PRE && c == 0) {
+#pragma unroll
+        for (int kt = 0; kt < NKT1; ++kt) stepA(kt, wA0[kt]);
+      } else if constexpr (PRE && c == 1) {
 #pragma unroll
         for (int kt = 0; kt < NKT1; ++kt) stepA(kt, wA1[kt]);
       } else {

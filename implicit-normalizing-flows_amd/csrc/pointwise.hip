@@ -920,26 +920,31 @@ int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, 
 // power-series combine: tr_k[b] = (float) sum_chunks partial[k][b][c];  out[b] = sum_k fl(c_k * tr_k)
 // accumulated in fp32 in k order like `logdetgrad = logdetgrad + delta` (implicit_block.py:421-426).
 // ------------------------------------------------------------------------------------------
+// one 128-thread workgroup per sample: thread k sums term k's chunks (in chunk order, fp64) and forms fl(c_k * tr_k);
+// thread 0 then accumulates the terms in k order in fp32 (the same operations as a serial loop, so the same bits)
 __global__ void series_combine_kernel(const double* partials, CoeffTable ct, int n_terms, int batch, int nchunk,
                                       float* out) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= batch) return;
-  float acc = 0.f;
-  for (int k = 0; k < n_terms; ++k) {
+  const int b = blockIdx.x, k = threadIdx.x;
+  __shared__ float term[128];
+  if (k < n_terms) {
     double s = 0.0;
     const double* p = partials + ((long)k * batch + b) * nchunk;
     for (int c = 0; c < nchunk; ++c) s += p[c];
-    acc = acc + ct.c[k] * (float)s;
+    term[k] = ct.c[k] * (float)s;
   }
-  out[b] = acc;
+  __syncthreads();
+  if (k == 0) {
+    float acc = 0.f;
+    for (int j = 0; j < n_terms; ++j) acc = acc + term[j];
+    out[b] = acc;
+  }
 }
 int launch_series_combine(const double* partials, const float* coeff_host, int n_terms, int batch, int nchunk,
                           float* out, hipStream_t s) {
   if (n_terms > 128) return INF_ERR_UNSUPPORTED;
   CoeffTable ct;
   for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
-  hipLaunchKernelGGL(series_combine_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, partials, ct, n_terms, batch,
-                     nchunk, out);
+  hipLaunchKernelGGL(series_combine_kernel, dim3(batch), dim3(128), 0, s, partials, ct, n_terms, batch, nchunk, out);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

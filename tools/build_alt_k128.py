@@ -6,6 +6,7 @@ shipped: the product source stays untouched; a patched copy is compiled into gpu
       d1l2   the same for d1
       nod2   no d2 loads at all (multiplier 1)
       nod1   no d1 loads at all (multiplier 1)
+      dsyncN first-round workgroups of every other CU group start N k-cycles late (desynchronised bursts)
       sub    INFLOW_K128_SUBSTAMPS: stamps inside chunk 1 and phase C (results unchanged; sched_barrier fences)
 Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py, INFLOW_FUSED_TIMING=1 for the phase stamps).
 """
@@ -32,6 +33,14 @@ def patch(src, variants):
     if 'nod1' in variants:
         rep.append(('for (int j = 0; j < 4; ++j) d1v[b][j] = q[j];',
                     'for (int j = 0; j < 4; ++j) d1v[b][j] = f32x4{1.f, 1.f, 1.f, 1.f}; (void)q;'))
+    for v in variants:
+        if v.startswith('dsync'):      # first-round workgroups on half the CUs start D k-cycles late (results unchanged)
+            d = int(v[5:]) * 1000
+            rep.append(('  KSTAMP(0);\n',
+                        '  if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1)) {\n'
+                        '    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();\n'
+                        '    while (__builtin_amdgcn_s_memtime() - t0_ < %dull) __builtin_amdgcn_s_sleep(64);\n'
+                        '  }\n  KSTAMP(0);\n' % d))
     if 'sub' in variants:
         src = '#define INFLOW_K128_SUBSTAMPS 1\n' + src
     for old, new in rep:
