@@ -7,6 +7,7 @@ shipped: the product source stays untouched; a patched copy is compiled into gpu
       nod2   no d2 loads at all (multiplier 1)
       nod1   no d1 loads at all (multiplier 1)
       dsyncN first-round workgroups of every other CU group start N k-cycles late (desynchronised bursts)
+      DNAME=V  #define NAME V ahead of the source (the product's compile-time switches)
       sub    INFLOW_K128_SUBSTAMPS: stamps inside chunk 1 and phase C (results unchanged; sched_barrier fences)
 Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py, INFLOW_FUSED_TIMING=1 for the phase stamps).
 """
@@ -41,6 +42,9 @@ def patch(src, variants):
                         '    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();\n'
                         '    while (__builtin_amdgcn_s_memtime() - t0_ < %dull) __builtin_amdgcn_s_sleep(64);\n'
                         '  }\n  KSTAMP(0);\n' % d))
+    for v in variants:
+        if v.startswith('D') and '=' in v:  # compile-time switch of the product source, e.g. DK128_EARLY_W3=0
+            src = '#define %s %s\n' % tuple(v[1:].split('=')) + src
     if 'sub' in variants:
         src = '#define INFLOW_K128_SUBSTAMPS 1\n' + src
     for old, new in rep:
