@@ -61,6 +61,14 @@ __device__ __forceinline__ float act_d(float a, float sp) {
   else return 1.f;
 }
 
+// A kernel-constant scalar (scale exponent, activation beta) read through the scalar cache: an s_load counts on
+// lgkmcnt, so it does not queue behind the wave's in-flight vector loads (fused313k.hip: a global_load of the
+// phase-A exponent issued after the d2 requests waited for the whole d2 burst).  Read-only.
+template <typename T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)(p);
+}
+
 // ---- reductions ---------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -159,14 +159,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   // Series chaining: the input is the previous VJP's packed taps; the tap sum, the preact swish'
   // multiplier and that term's trace partial (conv_out's OM_VJP work) happen here instead.
   const float* in = a.in + (long)img * a.C * P;
-  const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+  const float pre_sp = a.pre_beta ? softplus_f(ldc(a.pre_beta)) : 0.f;
   double dacc = 0.0;
   if (pr.dbg & 8) {
   } else if (a.in_taps) {
     const float* ytap = a.in_taps + (long)img * a.M3 * P;
     const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
     const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
-    const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
+    const float msp = a.vmul_x ? softplus_f(ldc(a.vmul_beta)) : 0.f;
     // Up to 4 halo elements per pass with unconditional (clamped-address) loads, all issued before any
     // is used: 44 loads in flight per thread instead of one bounds-checked chain per element.  The pass
     // width NU is wave-uniform and a compile-time constant per branch (a runtime slot guard lets the
@@ -351,7 +351,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int w = 0; w < NW; ++w) m_ = fmaxf(m_, hmax[w]);
       const int sc = h3_scale_exp(m_);
       sA = __builtin_amdgcn_ldexpf(1.f, sc);
-      eA = -(sc + a.Ah_exp[0]);
+      eA = -(sc + ldc(a.Ah_exp));
     }
     auto ld3 = [&](int m, int kt, u32x4 (&o)[NPAC]) { ldw<NPAC>(A1w, (long)(rbw + m) * nkt + kt, lane, o); };
     // B operand (im2col gather from the halo tile) one K tile ahead: its LDS reads and split overlap
@@ -463,7 +463,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   STAMP(2);
   // epilogue A -> t (LDS); SAVE: d1 -> HBM
   {
-    const float sp1 = (MODE != MODE_VJP) ? softplus_f(*a.beta1) : 0.f;
+    const float sp1 = (MODE != MODE_VJP) ? softplus_f(ldc(a.beta1)) : 0.f;
     float cm[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) cm[b] = 0.f;
@@ -506,7 +506,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   if constexpr (H3) {
     constexpr int nkt = HID / 16;
     const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);   // (phase-B planes: a.A2h)
-    const int sw = a.Ah_exp[1];
+    const int sw = ldc(a.Ah_exp + 1);
     float hs[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -698,7 +698,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   STAMP(4);
   WSTAMP(8);
   if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) {
-    const float sp2 = softplus_f(*a.beta2);
+    const float sp2 = softplus_f(ldc(a.beta2));
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -722,7 +722,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           load_d(a.d1, m, b, dmul[m][b]);
         }
     }
-    const float sp2 = (MODE != MODE_VJP) ? softplus_f(*a.beta2) : 0.f;
+    const float sp2 = (MODE != MODE_VJP) ? softplus_f(ldc(a.beta2)) : 0.f;
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -772,7 +772,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       for (int w = 0; w < NW; ++w) m_ = fmaxf(m_, cmax[w * F_BN + b * 32 + li]);
       const int sc = h3_scale_exp(m_);
       S = __builtin_amdgcn_ldexpf(1.f, sc);
-      e = -(sc + a.Ah_exp[2]);
+      e = -(sc + ldc(a.Ah_exp + 2));
     };
 
     // -------------------------------------------------------------- phase C: taps, K = HID

@@ -69,6 +69,7 @@ __device__ __forceinline__ void split4h(float v0, float v1, float v2, float v3, 
 }
 
 constexpr int kb_seg(int W) { return W < KB_BN ? W : KB_BN; }
+
 }  // namespace
 
 // 128-pixel tiles fit: whole image rows (or a 128-wide row segment), halo + im2col table + chunk buffer
@@ -159,20 +160,28 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   // loads, so phase A's MFMAs run while the d2 burst arrives (only its epilogue waits); chunk 1's (<= 4 tiles) in the
   // last K step of phase B of chunk 0, ahead of chunk 1's d2
   constexpr int NKT1 = CT ? (9 * CT + 15) / 16 : 0;
-  constexpr bool PRE_A0 = NKT1 > 0 && NKT1 <= 4;
+#ifndef K128_PRE_A0_MAX
+#define K128_PRE_A0_MAX 4
+#endif
+#ifndef K128_LATE_D2
+#define K128_LATE_D2 0
+#endif
+  constexpr bool PRE_A0 = NKT1 > 0 && NKT1 <= K128_PRE_A0_MAX;
   constexpr bool PRE_A1 = NKT1 > 0 && NKT1 <= 4;
   u32x4 wA0[PRE_A0 ? NKT1 : 1][2];
   u32x4 wA1[PRE_A1 ? NKT1 : 1][2];
   bool early_pending = true;                        // wave-uniform
   auto issue_early = [&]() {
+    __builtin_amdgcn_sched_barrier(0);              // (in program order: after the staging loads)
     if constexpr (PRE_A0) {
 #pragma unroll
       for (int kt = 0; kt < NKT1; ++kt) ldw2(reinterpret_cast<const u32x4*>(a.A1h), (long)wid * NKT1 + kt, lane, wA0[kt]);
     }
     loadD2(0, 0, KB_NB);
+    __builtin_amdgcn_sched_barrier(0);
     early_pending = false;
   };
-  if (!PRE_A0 || !a.in_taps) issue_early();         // (without preloaded weights phase A would wait for d2 anyway)
+  if ((!PRE_A0 && !(K128_LATE_D2 && CT)) || !a.in_taps) issue_early();         // (without preloaded weights phase A would wait for d2 anyway)
 
   // ---- stage the input halo tile (series chaining: tap sum, preact swish', trace partial / Neumann acc) ----
   float hmx = 0.f;
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       const float* ytap = a.in_taps + (long)img * M3 * P;
       const float* mx = a.vmul_x ? a.vmul_x + (long)img * C * P : nullptr;
       const float* ep = a.dot_eps ? a.dot_eps + (long)img * C * P : nullptr;
-      const float msp = a.vmul_x ? softplus_f(*a.vmul_beta) : 0.f;
+      const float msp = a.vmul_x ? softplus_f(ldc(a.vmul_beta)) : 0.f;
       const float* mxp = mx ? mx : ytap;
       const float* epp = ep ? ep : ytap;
       float* accw = a.acc_w ? a.acc_w + (long)img * C * P : nullptr;
@@ -234,16 +243,17 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           if (i < vhz) vh[i] = v;
         }
       };
-      constexpr int SU = 4;
+      constexpr int SU = (K128_LATE_D2 && CT) ? 5 : 4;
       for (int i0 = tid; i0 < vhz; i0 += KB_NT * SU) {
         const int nu = min(SU, (vhz - (i0 - tid) + KB_NT - 1) / KB_NT);     // wave-uniform
-        if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
+        if (nu >= 5) pass(std::integral_constant<int, SU>(), i0);
+        else if (nu == 4) pass(std::integral_constant<int, 4>(), i0);
         else if (nu == 3) pass(std::integral_constant<int, 3>(), i0);
         else if (nu == 2) pass(std::integral_constant<int, 2>(), i0);
         else pass(std::integral_constant<int, 1>(), i0);
       }
     } else {
-      const float pre_sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+      const float pre_sp = a.pre_beta ? softplus_f(ldc(a.pre_beta)) : 0.f;
       for (int i = tid; i < vhz; i += KB_NT) {
         float v = 0.f;
         if (i < vhn) {
@@ -300,14 +310,14 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, hmax[w]);
     const int sc = h3_scale_exp(m_);
     sA = __builtin_amdgcn_ldexpf(1.f, sc);
-    eA = -(sc + a.Ah_exp[0]);
+    eA = -(sc + ldc(a.Ah_exp));
   }
   const u32x4* A1h = reinterpret_cast<const u32x4*>(a.A1h);
   const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);
   const u32x4* A3p = reinterpret_cast<const u32x4*>(a.A3p);
   const int nkt1 = K1pad / 16;
-  const int ew = a.Ah_exp[1];
-  const float sp1 = VJP ? 0.f : softplus_f(*a.beta1), sp2 = VJP ? 0.f : softplus_f(*a.beta2);
+  const int ew = ldc(a.Ah_exp + 1);
+  const float sp1 = VJP ? 0.f : softplus_f(ldc(a.beta1)), sp2 = VJP ? 0.f : softplus_f(ldc(a.beta2));
 
   // writes this wave's values of one 32-row block (rows kt0 * 16 .. + 31 of the chunk) and column block b
   // into the chunk buffer: accumulator group g holds rows 8g + 4 lh + q, which consumer lane 32 (g & 1) + li
@@ -574,7 +584,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       split2h(x, S, bh[kk][b], bl[kk][b]);
     }
   }
-  const int ew3 = a.Ah_exp[2];
+  const int ew3 = ldc(a.Ah_exp + 2);
   int eC[KB_NB];
 #pragma unroll
   for (int b = 0; b < KB_NB; ++b) eC[b] = -(sw[b] + ew3);
