@@ -160,13 +160,8 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   // loads, so phase A's MFMAs run while the d2 burst arrives (only its epilogue waits); chunk 1's (<= 4 tiles) in the
   // last K step of phase B of chunk 0, ahead of chunk 1's d2
   constexpr int NKT1 = CT ? (9 * CT + 15) / 16 : 0;
-#ifndef K128_PRE_A0_MAX
-#define K128_PRE_A0_MAX 4
-#endif
-#ifndef K128_LATE_D2
-#define K128_LATE_D2 0
-#endif
-  constexpr bool PRE_A0 = NKT1 > 0 && NKT1 <= K128_PRE_A0_MAX;
+  constexpr bool PRE_A0 = NKT1 > 0 && NKT1 <= 4;     // (<= 8 at scale 1 spills; d2 after the staging loads without
+                                                      // preloaded weights measured neutral there)
   constexpr bool PRE_A1 = NKT1 > 0 && NKT1 <= 4;
   u32x4 wA0[PRE_A0 ? NKT1 : 1][2];
   u32x4 wA1[PRE_A1 ? NKT1 : 1][2];
@@ -181,7 +176,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     __builtin_amdgcn_sched_barrier(0);
     early_pending = false;
   };
-  if ((!PRE_A0 && !(K128_LATE_D2 && CT)) || !a.in_taps) issue_early();         // (without preloaded weights phase A would wait for d2 anyway)
+  if (!PRE_A0 || !a.in_taps) issue_early();         // (without preloaded weights phase A would wait for d2 anyway)
 
   // ---- stage the input halo tile (series chaining: tap sum, preact swish', trace partial / Neumann acc) ----
   float hmx = 0.f;
@@ -243,11 +238,10 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
           if (i < vhz) vh[i] = v;
         }
       };
-      constexpr int SU = (K128_LATE_D2 && CT) ? 5 : 4;
+      constexpr int SU = 4;
       for (int i0 = tid; i0 < vhz; i0 += KB_NT * SU) {
         const int nu = min(SU, (vhz - (i0 - tid) + KB_NT - 1) / KB_NT);     // wave-uniform
-        if (nu >= 5) pass(std::integral_constant<int, SU>(), i0);
-        else if (nu == 4) pass(std::integral_constant<int, 4>(), i0);
+        if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
         else if (nu == 3) pass(std::integral_constant<int, 3>(), i0);
         else if (nu == 2) pass(std::integral_constant<int, 2>(), i0);
         else pass(std::integral_constant<int, 1>(), i0);
