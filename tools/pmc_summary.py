@@ -31,7 +31,7 @@ def main():
     ap.add_argument('--out', default='profiles/pmc_dominant_kernel.json')
     # the dominant kernel: the 128-pixel K-chunked VJP (tag 532); the 64-pixel one is
     # --prefix 'void inf::net313_kernel<2, 2' --tag 502 --kernel 'net313_kernel<VJP>'
-    ap.add_argument('--prefix', default='void inf::net313k_kernel<2>')
+    ap.add_argument('--prefix', default='void inf::net313k_kernel<2,')
     ap.add_argument('--tag', type=int, default=532)
     ap.add_argument('--kernel', default='net313k_kernel<VJP>')
     ap.add_argument('--config', default='cifar10')
