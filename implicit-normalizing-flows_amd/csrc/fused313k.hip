@@ -33,8 +33,8 @@
 // d1 / d2 are read in the 64-pixel kernel's fragment layout (the SAVE launches of the pair write them):
 // 128-pixel tile t covers 64-pixel tiles 2t, 2t + 1.
 //
-// The geometry (C, W) of the CIFAR scales is a template parameter (CT, WT; 0 = from the arguments), so the halo
-// index arithmetic, phase A's K loop and phase C's row-block loop are compile-time.
+// The geometry (C, W) of the CIFAR-10 and CelebA-HQ 256 scales is a template parameter (CT, WT; 0 = from the
+// arguments), so the halo index arithmetic, phase A's K loop and phase C's row-block loop are compile-time.
 #include <type_traits>
 
 #include "kernels.h"
@@ -646,6 +646,8 @@ int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s) {
   if (mode != MODE_VJP && mode != MODE_EVAL) return INF_ERR_UNSUPPORTED;
   if (C == 3 && W == 32) K128_GEO(3, 32);            // CIFAR-10 scale 0
   else if (C == 12 && W == 16) K128_GEO(12, 16);     // CIFAR-10 scale 1
+  else if (C == 3 && W == 256) K128_GEO(3, 256);     // CelebA-HQ 256 scale 0
+  else if (C == 12 && W == 128) K128_GEO(12, 128);   // CelebA-HQ 256 scale 1
   else K128_GEO(0, 0);
 #undef K128_GEO
   INF_CHECK_LAUNCH();

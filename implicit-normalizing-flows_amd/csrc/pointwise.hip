@@ -385,7 +385,23 @@ __global__ __launch_bounds__(256) void broyden_p1(BroydenArgs a, int nchunk) {
   }
 }
 
-__global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, double* part2) {
+// Large d (CelebA-HQ: 192 chunks per sample): the chunk partials are summed once per sample into chunk 0's slot (the
+// same serial order the consumers used) instead of by every block of the sample; the consumers then read nsum = 1.
+// part[b][c][ld]: column col(j) = j < m1 ? j : off2 + j - m1, j < ncol
+__global__ __launch_bounds__(64) void br_sum_chunks(double* part, int nchunk, int ld, int m1, int off2, int ncol,
+                                                    const int* active) {
+  const int b = blockIdx.x;
+  if (active && !active[b]) return;
+  for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
+    const int col = j < m1 ? j : off2 + (j - m1);
+    double* p = part + (long)b * nchunk * ld + col;
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) s += p[(long)c * ld];
+    p[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, int nsum, double* part2) {
   __shared__ double red[16];
   __shared__ float coef[2 * BR_TMAX];
   const int b = blockIdx.y, ch = blockIdx.x;
@@ -393,7 +409,7 @@ __global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, dou
   for (int j = threadIdx.x; j < 2 * a.m; j += blockDim.x) {
     const int jj = j < a.m ? j : a.T + (j - a.m);
     double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += a.part[((long)b * nchunk + c) * 2 * a.T + jj];
+    for (int c = 0; c < nsum; ++c) s += a.part[((long)b * nchunk + c) * 2 * a.T + jj];
     coef[j] = (float)s;   // a_j (j < m) then c_j
   }
   __syncthreads();
@@ -416,14 +432,14 @@ __global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, dou
   if (threadIdx.x == 0) part2[(long)b * nchunk + ch] = den;
 }
 
-__global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, const double* part2, double* part3) {
+__global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, int nsum, const double* part2, double* part3) {
   __shared__ double red[16];
   __shared__ float denf;
   const int b = blockIdx.y, ch = blockIdx.x;
   if (a.active && !a.active[b]) return;
   if (threadIdx.x == 0) {
     double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += part2[(long)b * nchunk + c];
+    for (int c = 0; c < nsum; ++c) s += part2[(long)b * nchunk + c];
     denf = (float)s;
   }
   __syncthreads();
@@ -453,7 +469,7 @@ __global__ __launch_bounds__(256) void broyden_p3(BroydenArgs a, int nchunk, con
   }
 }
 
-__global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, const double* part3) {
+__global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, int nsum, const double* part3) {
   __shared__ float ej[BR_TMAX];
   const int b = blockIdx.y, ch = blockIdx.x;
   if (a.active && !a.active[b]) {
@@ -468,7 +484,7 @@ __global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, con
   }
   for (int j = threadIdx.x; j < a.ncols; j += blockDim.x) {
     double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += part3[((long)b * nchunk + c) * a.T + j];
+    for (int c = 0; c < nsum; ++c) s += part3[((long)b * nchunk + c) * a.T + j];
     ej[j] = (float)s;
   }
   __syncthreads();
@@ -497,15 +513,20 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   dim3 grid(nchunk, a.batch);
   double* part2 = a.part + (long)a.batch * nchunk * 2 * a.T;
   double* part3 = part2 + (long)a.batch * nchunk;
+  const bool pre = nchunk >= 32;       // (small nchunk: the consumers' own sums are cheaper than three more launches)
+  const int nsum = pre ? 1 : nchunk;
   if (a.m > 0) {
     hipLaunchKernelGGL(broyden_p1, grid, dim3(256), 0, s, a, nchunk);
     INF_CHECK_LAUNCH();
+    if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, a.part, nchunk, 2 * a.T, a.m, a.T, 2 * a.m, a.active);
   }
-  hipLaunchKernelGGL(broyden_p2, grid, dim3(256), 0, s, a, nchunk, part2);
+  hipLaunchKernelGGL(broyden_p2, grid, dim3(256), 0, s, a, nchunk, nsum, part2);
   INF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, part2, part3);
+  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, part2, nchunk, 1, 1, 0, 1, a.active);
+  hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, nsum, part2, part3);
   INF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, part3);
+  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, part3, nchunk, a.T, a.ncols, 0, a.ncols, a.active);
+  hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, nsum, part3);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
@@ -920,20 +941,23 @@ int launch_fwdmode_act(float* a, float* deriv, int d_out, int batch, int ntang, 
 // power-series combine: tr_k[b] = (float) sum_chunks partial[k][b][c];  out[b] = sum_k fl(c_k * tr_k)
 // accumulated in fp32 in k order like `logdetgrad = logdetgrad + delta` (implicit_block.py:421-426).
 // ------------------------------------------------------------------------------------------
-// one 128-thread workgroup per sample: thread k sums term k's chunks (in chunk order, fp64) and forms fl(c_k * tr_k);
-// thread 0 then accumulates the terms in k order in fp32 (the same operations as a serial loop, so the same bits)
-__global__ void series_combine_kernel(const double* partials, CoeffTable ct, int n_terms, int batch, int nchunk,
-                                      float* out) {
-  const int b = blockIdx.x, k = threadIdx.x;
+// one 256-thread workgroup per sample: wave w sums terms k = w, w + 4, ... (its lanes over the term's chunks in fp64,
+// a fixed shuffle tree) and forms fl(c_k * tr_k); thread 0 then accumulates the terms in k order in fp32, i.e.
+// logdetgrad + delta with torch's two roundings per term (CelebA-HQ 256 has 512 chunks per term: a serial loop per
+// term took 73 us)
+__global__ __launch_bounds__(256) void series_combine_kernel(const double* partials, CoeffTable ct, int n_terms,
+                                                             int batch, int nchunk, float* out) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __shared__ float term[128];
-  if (k < n_terms) {
-    double s = 0.0;
+  for (int k = w; k < n_terms; k += 4) {
     const double* p = partials + ((long)k * batch + b) * nchunk;
-    for (int c = 0; c < nchunk; ++c) s += p[c];
-    term[k] = ct.c[k] * (float)s;
+    double s = 0.0;
+    for (int c = lane; c < nchunk; c += 64) s += p[c];
+    s = wave_sum(s);
+    if (lane == 0) term[k] = ct.c[k] * (float)s;
   }
   __syncthreads();
-  if (k == 0) {
+  if (threadIdx.x == 0) {
     float acc = 0.f;
     for (int j = 0; j < n_terms; ++j) acc = acc + term[j];
     out[b] = acc;
@@ -944,7 +968,7 @@ int launch_series_combine(const double* partials, const float* coeff_host, int n
   if (n_terms > 128) return INF_ERR_UNSUPPORTED;
   CoeffTable ct;
   for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
-  hipLaunchKernelGGL(series_combine_kernel, dim3(batch), dim3(128), 0, s, partials, ct, n_terms, batch, nchunk, out);
+  hipLaunchKernelGGL(series_combine_kernel, dim3(batch), dim3(256), 0, s, partials, ct, n_terms, batch, nchunk, out);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
