@@ -209,9 +209,10 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
             const int y2 = min(max(yq + tp / 3 - 1, 0), a.H - 1), x2 = min(max(xq + tp % 3 - 1, 0), W - 1);
             tv[u][tp] = yc[(long)tp * P + y2 * W + x2];
           }
-          xm[u] = mxp[ee];
-          ev[u] = epp[ee];
-          wv[u] = awp[ee];
+          // (side inputs only where the net has them: a dummy load still costs a slot in the wave's load queue)
+          xm[u] = mx ? mxp[ee] : 0.f;
+          ev[u] = ep ? epp[ee] : 0.f;
+          wv[u] = accw ? awp[ee] : 0.f;
         }
         if (early_pending && i0 - tid + KB_NT * NU >= vhz) issue_early();   // after the last pass's loads
 #pragma unroll
@@ -590,7 +591,6 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   u32x4 w3[4][2];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) ldw2(A3p, 4 * wid + kk, lane, w3[kk]);
-  __syncthreads();                                   // every wave is done reading the phase-B chunk buffer
 #pragma unroll 1
   for (int rb = 0; rb < nrb; ++rb) {
     f32x16 cacc[KB_NB];
@@ -604,6 +604,9 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       for (int b = 0; b < KB_NB; ++b) cacc[b] = mfma_h3(w3[kk], bh[kk][b], bl[kk][b], cacc[b]);
       if (rb + 1 < nrb) ldw2(A3p, (long)(rb + 1) * 32 + 4 * wid + kk, lane, w3[kk]);   // the next row block's
     }
+    // the first partials overwrite the phase-B chunk buffer: every wave must be done reading it (after this wave's
+    // MFMAs, so a wave whose d1 arrived early contracts while the others wait for theirs)
+    if (rb == 0) __syncthreads();
 #pragma unroll
     for (int b = 0; b < KB_NB; ++b)
 #pragma unroll
