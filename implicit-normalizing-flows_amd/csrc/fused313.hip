@@ -1143,7 +1143,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // VJP / EVAL variant policy (per net, INF_OPT_FUSED_K128): 0 the 64-pixel kernel only, 1 the 128-pixel
   // K-chunked kernel where its grid still covers every CU (default), 2 wherever it fits (tests)
   const int k128_pol = a0.k128;
-  const bool k128 = k128_pol && H3_AC && h3_args && (mode == MODE_VJP || mode == MODE_EVAL) && var == V64 && force_bn == 0 &&
+  const bool k128 = k128_pol && H3_AC && h3_args && var == V64 && force_bn == 0 &&
                     force_var < 0 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
                     (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
   const int tbn = k128 ? 128 : bn;
@@ -1187,8 +1187,9 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
     }
     if (prof) {
       const double npx = (double)nnets * a0.B * P;
-      const double f = 2.0 * hid * 9.0 * a0.C * 2.0 + 2.0 * hid * hid;
-      const double bytes = 4.0 * npx * (a0.C + (mode == MODE_VJP ? 2.0 * hid : 0.0) + 9.0 * a0.C);
+      const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
+      const double f = 2.0 * hid * 9.0 * a0.C + 2.0 * hid * hid + fC;
+      const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
       prof_end_launch(s, 530 + mode, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
     }
     return INF_OK;

@@ -85,10 +85,14 @@ int net313k_fits(int hid, int C, int H, int W) {
   return need <= KB_LDS;
 }
 
-// MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2))
+// MODE_VJP: v^T J (epilogues x d2, x d1); MODE_EVAL: the net's forward value (epilogues swish(. + b1 / b2));
+// MODE_SAVE / MODE_EVALSAVE: the forward that writes d1, d2 (SAVE without phase C), as in fused313.hip
 template <int MODE, int CT, int WT>
 __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   constexpr bool VJP = MODE == MODE_VJP;
+  // forward modes that also write the activation derivatives d1 = swish'(a1), d2 = swish'(a2) in the 64-pixel kernel's
+  // fragment order (the order this kernel's VJP reads them in); MODE_SAVE stops after phase B
+  constexpr bool SAVE = MODE == MODE_SAVE || MODE == MODE_EVALSAVE;
   const int bx = pr.reverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
   const int sel = bx >= pr.nb0 ? 1 : 0;
   const Net313Args& a = pr.a[sel];
@@ -402,11 +406,15 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
             va[b][4 * j + 2] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 2], eA) * d.z;
             va[b][4 * j + 3] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 3], eA) * d.w;
           } else {                                   // forward: swish(a1 + b1), rows of accumulator group j
+            f32x4 dd;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int row = rbA * 32 + q + 8 * j + 4 * lh;
-              va[b][4 * j + q] = swish_fast_f(__builtin_amdgcn_ldexpf(ac[g][4 * j + q], eA) + a.b1[row], sp1);
+              const float z = __builtin_amdgcn_ldexpf(ac[g][4 * j + q], eA) + a.b1[row];
+              va[b][4 * j + q] = swish_fast_f(z, sp1);
+              if constexpr (SAVE) dd[q] = swish_fast_d(z, sp1);
             }
+            if constexpr (SAVE) const_cast<f32x4*>(dptr(a.d1, rbA, b))[j] = dd;
           }
         }
 #pragma unroll
@@ -535,10 +543,18 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     for (int b = 0; b < KB_NB; ++b) {
       const int e = -(scB[b] + ew);
       if constexpr (!VJP) {                        // forward: swish(a2 + b2)
+        float dd[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = (2 * wid + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          acc[m][b][r] = swish_fast_f(__builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row], sp2);
+          const float z = __builtin_amdgcn_ldexpf(acc[m][b][r], e) + a.b2[row];
+          acc[m][b][r] = swish_fast_f(z, sp2);
+          if constexpr (SAVE) dd[r] = swish_fast_d(z, sp2);
+        }
+        if constexpr (SAVE) {
+          f32x4* q = const_cast<f32x4*>(dptr(a.d2, 2 * wid + m, b));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) q[j] = f32x4{dd[4 * j], dd[4 * j + 1], dd[4 * j + 2], dd[4 * j + 3]};
         }
         continue;
       }
@@ -553,6 +569,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     }
     if (m == 0) KSUB(6);
   }
+  if constexpr (MODE == MODE_SAVE) return;          // (the derivatives are written; no taps)
   // ------------------------------------------------ phase C from registers
   // column scale over this wave's 64 rows; t2 split in place into the B operands of its 4 K tiles
   // (K tile kk = 2 m + t of the wave = global K tile 4 wid + kk; slot s = 4a + q <- acc[m][b][8t + s])
@@ -644,9 +661,11 @@ int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s) {
 #define K128_GEO(CT_, WT_)                                                                                        \
   do {                                                                                                            \
     if (mode == MODE_VJP) hipLaunchKernelGGL((net313k_kernel<MODE_VJP, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr); \
-    else hipLaunchKernelGGL((net313k_kernel<MODE_EVAL, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr);              \
+    else if (mode == MODE_EVAL) hipLaunchKernelGGL((net313k_kernel<MODE_EVAL, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr); \
+    else if (mode == MODE_SAVE) hipLaunchKernelGGL((net313k_kernel<MODE_SAVE, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr); \
+    else hipLaunchKernelGGL((net313k_kernel<MODE_EVALSAVE, CT_, WT_>), dim3(nb), dim3(KB_NT), 0, s, pr);          \
   } while (0)
-  if (mode != MODE_VJP && mode != MODE_EVAL) return INF_ERR_UNSUPPORTED;
+  if (mode != MODE_VJP && mode != MODE_EVAL && mode != MODE_SAVE && mode != MODE_EVALSAVE) return INF_ERR_UNSUPPORTED;
   if (C == 3 && W == 32) K128_GEO(3, 32);            // CIFAR-10 scale 0
   else if (C == 12 && W == 16) K128_GEO(12, 16);     // CIFAR-10 scale 1
   else if (C == 3 && W == 256) K128_GEO(3, 256);     // CelebA-HQ 256 scale 0
