@@ -9,7 +9,8 @@
 
 namespace inf {
 
-constexpr int OUT_CH = 1024;   // elements per block in conv_out (256 threads x 4)
+constexpr int OUT_CH = 1024;   // elements per block in conv_out: one per thread (4 per thread of 256 was latency-bound,
+                               // 19 us per CIFAR residual at B=64)
 
 // power-series coefficients, passed by value as a kernel argument
 struct CoeffTable {
@@ -29,12 +30,12 @@ int out_nchunk(int per_sample) { return (per_sample + OUT_CH - 1) / OUT_CH; }
 //   OM_VJP   : out0 = v = s (* swish'(x_in) for preact nets);  partial += v * eps
 // ------------------------------------------------------------------------------------------
 template <int KS>
-__global__ __launch_bounds__(256) void conv_out_kernel(OutArgs a) {
+__global__ __launch_bounds__(OUT_CH) void conv_out_kernel(OutArgs a) {
   __shared__ double red[16];
   const int b = blockIdx.y, chunk = blockIdx.x;
   const int P = a.H * a.W, per = a.C * P;
   const long ybase = (long)b * a.y_sample, ebase = (long)b * per;
-  const float sp = a.pre_beta ? softplus_f(*a.pre_beta) : 0.f;
+  const float sp = a.pre_beta ? softplus_f(ldc(a.pre_beta)) : 0.f;
   const int lo = chunk * OUT_CH, hi = min(per, lo + OUT_CH);
   double acc = 0.0;
   for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
@@ -91,9 +92,9 @@ int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
   if (a.ks == 1)
-    hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(OUT_CH), 0, s, a);
   else
-    hipLaunchKernelGGL(conv_out_kernel<3>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(conv_out_kernel<3>, grid, dim3(OUT_CH), 0, s, a);
   INF_CHECK_LAUNCH();
   if (prof) {
     // bytes: the Y rows read (9 taps or 1) + ~3 per-element vectors in/out
@@ -105,7 +106,7 @@ int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
 
 // First Broyden residual from the cached f(0) (conv nets): v = f0[i] for every sample,
 // g = (x_embed - v) - z exactly as conv_out's OM_RESID, fcur = v, per-sample partial sums of g^2.
-__global__ __launch_bounds__(256) void resid_bcast_kernel(const float* f0, const float* xemb, const float* z, float* g,
+__global__ __launch_bounds__(OUT_CH) void resid_bcast_kernel(const float* f0, const float* xemb, const float* z, float* g,
                                                           float* fcur, double* partial, int per, int nchunk) {
   __shared__ double red[16];
   const int b = blockIdx.y, chunk = blockIdx.x;
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void resid_bcast_kernel(const float* f0, const
 }
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s) {
-  hipLaunchKernelGGL(resid_bcast_kernel, dim3(out_nchunk(per), batch), dim3(256), 0, s, f0, xemb, z, g, fcur,
+  hipLaunchKernelGGL(resid_bcast_kernel, dim3(out_nchunk(per), batch), dim3(OUT_CH), 0, s, f0, xemb, z, g, fcur,
                      partial, per, nchunk);
   INF_CHECK_LAUNCH();
   return INF_OK;
