@@ -81,7 +81,7 @@ int net313k_fits(int hid, int C, int H, int W) {
   if (9 * C > 256) return 0;                      // phase A: at most 16 K tiles
   const int rows = KB_BN / seg;
   const long k1pad = (9L * C + 15) / 16 * 16;
-  const long need = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
+  const long need = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + 4 + k1pad + (long)C * (rows + 2) * (seg + 2) + (long)rows * (seg + 2);
   return need <= KB_LDS;
 }
 
@@ -132,12 +132,13 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   const int RH = rows + 2, CW = seg + 2;
   const int vhn = C * RH * CW;
   const int vhz = vhn + rows * CW;                  // zero run for the K-padding rows of phase A
-  // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] | trace partials [NW] (fp64) | koff | halo
+  // LDS: chunk buffer | column maxima [NW][BN] | halo maxima [8] | trace partials [NW] (fp64) | flags [4] | koff | halo
   u32x4* cb = reinterpret_cast<u32x4*>(smem);
   float* cmax = smem + KB_CHUNK;
   float* hmax = cmax + KB_NW * KB_BN;
   double* red = reinterpret_cast<double*>(hmax + 8);
-  int* koff = reinterpret_cast<int*>(red + KB_NW);
+  int* ovf = reinterpret_cast<int*>(red + KB_NW);   // [0]: chunk 1's fast-path overflow flag
+  int* koff = ovf + 4;                               // (16-byte aligned for the int4 reads)
   float* vh = reinterpret_cast<float*>(koff + K1pad);
 
   // d1 / d2 in the 64-pixel kernel's fragment order: 64-px tile (2 tile + b / 2), column (b & 1), row block rb
@@ -352,8 +353,11 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     const int rbA = 8 * c + wid;
     float va[KB_NB][16];
     // G column blocks b0 .. b0 + G - 1 over the K tiles in one sweep (each weight fragment used G times)
-    auto phaseA = [&](auto gc, auto bc) {
+    // FAST (chunk 1): put straight into the chunk buffer at chunk 0's column scale; `ovf` notes a value that would not
+    // fit fp16 there.  Otherwise: column maxima, and (chunk 1) the values parked for the exact-scale put.
+    auto phaseA = [&](auto gc, auto bc, auto fc) {
       constexpr int G = decltype(gc)::value, b0 = decltype(bc)::value;
+      constexpr bool FAST = decltype(fc)::value;
       f32x16 ac[G];
 #pragma unroll
       for (int g = 0; g < G; ++g)
@@ -417,6 +421,15 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
             if constexpr (SAVE) const_cast<f32x4*>(dptr(a.d1, rbA, b))[j] = dd;
           }
         }
+        if constexpr (FAST) {
+          const float S = __builtin_amdgcn_ldexpf(1.f, scB[b]);
+          bool o = false;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o = o || !(fabsf(va[b][r]) * S < 65504.f);   // (NaN too)
+          if (o) ovf[0] = 1;
+          put(2 * wid, b, va[b], S);
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) cm = fmaxf(cm, fabsf(va[b][r]));
         cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
@@ -428,52 +441,71 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       }
     };
     using I1 = std::integral_constant<int, 1>;
+    using FASTC = std::true_type;
+    using SLOWC = std::false_type;
+    // the exact column scales of the chunk, the accumulator moved to them (chunk 1), the put; after the column maxima
+    auto scale_put = [&]() {
+      if constexpr (c == 1) {                      // read back the parked values before the puts overwrite them
+#pragma unroll
+        for (int b = 0; b < KB_NB; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) va[b][r] = smem[wid * 4096 + (b * 16 + r) * 64 + lane];
+      }
+#pragma unroll
+      for (int b = 0; b < KB_NB; ++b) {
+        float m_ = 0.f;
+#pragma unroll
+        for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, cmax[w * KB_BN + b * 32 + li]);
+        int sc = h3_scale_exp(m_);
+        if constexpr (c == 1) {                    // chunk 1 stays within 2^60 of chunk 0
+          sc = min(max(sc, scB[b] - 60), scB[b] + 60);
+          const int de = sc - scB[b];
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], de);
+        }
+        scB[b] = sc;
+        put(2 * wid, b, va[b], __builtin_amdgcn_ldexpf(1.f, sc));
+      }
+    };
     if constexpr (c == 0) {
       // the phase-B accumulators are still zero constants: room for all four column blocks at once
-      phaseA(std::integral_constant<int, KB_NB>(), std::integral_constant<int, 0>());
+      phaseA(std::integral_constant<int, KB_NB>(), std::integral_constant<int, 0>(), SLOWC());
+      __syncthreads();    // column maxima visible
+      KSTAMP(2);
+      scale_put();
     } else {
-      // chunk 1: the phase-B accumulators hold 128 registers, so each column block's values are parked in LDS (in the
-      // 16 KiB of the chunk buffer this wave's put overwrites later) instead of registers; every wave must be done
-      // reading chunk 0's buffer first
-      __syncthreads();
+      // chunk 1 first tries chunk 0's column scales: the values go straight into the chunk buffer (no column maxima,
+      // no second barrier, the phase-B accumulators keep their scale).  A value beyond fp16 at that scale (a column
+      // whose chunk-1 maximum exceeds about twice its chunk-0 maximum) sends the whole tile through the exact-scale
+      // path, which parks each column block's values in the 16 KiB of the chunk buffer the same wave's put
+      // overwrites (the phase-B accumulators hold 128 registers).  Both put at one scale per column over the chunk;
+      // the fast one's error bound is relative to the column maximum over both chunks, as with a single 512-row scale.
+      if (tid == 0) ovf[0] = 0;
+      __syncthreads();    // every wave is done reading chunk 0's buffer; the overflow flag is reset
       // (d2 of column blocks 2 and 3 requested one pass ahead, in the registers of the blocks already used)
-      phaseA(I1(), std::integral_constant<int, 0>());
+      phaseA(I1(), std::integral_constant<int, 0>(), FASTC());
       KSUB(1);
       loadD2(1, 2, 3);
-      phaseA(I1(), std::integral_constant<int, 1>());
+      phaseA(I1(), std::integral_constant<int, 1>(), FASTC());
       loadD2(1, 3, 4);
-      phaseA(I1(), std::integral_constant<int, 2>());
-      phaseA(I1(), std::integral_constant<int, 3>());
+      phaseA(I1(), std::integral_constant<int, 2>(), FASTC());
+      phaseA(I1(), std::integral_constant<int, 3>(), FASTC());
       KSUB(2);
-    }
-    __syncthreads();      // column maxima visible; every wave is done reading the previous chunk buffer
-    if (c == 0) KSTAMP(2);
-    if (c == 1) KSUB(3);
-    // chunk column scales; chunk 1 stays within 2^60 of chunk 0 and the accumulator moves to its scale
-    if constexpr (c == 1) {                        // read back the parked values before the puts overwrite them
-#pragma unroll
-      for (int b = 0; b < KB_NB; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) va[b][r] = smem[wid * 4096 + (b * 16 + r) * 64 + lane];
-    }
-#pragma unroll
-    for (int b = 0; b < KB_NB; ++b) {
-      float m_ = 0.f;
-#pragma unroll
-      for (int w = 0; w < KB_NW; ++w) m_ = fmaxf(m_, cmax[w * KB_BN + b * 32 + li]);
-      int sc = h3_scale_exp(m_);
-      if constexpr (c == 1) {
-        sc = min(max(sc, scB[b] - 60), scB[b] + 60);
-        const int de = sc - scB[b];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], de);
+      __syncthreads();    // chunk buffer complete at chunk 0's scales; overflow flag visible
+      KSUB(3);
+      if (ovf[0] != 0 || (pr.dbg & 16)) {          // (block-uniform; INFLOW_FUSED_DBG bit 16 forces it for tests)
+        loadD2(1, 0, KB_NB);
+        phaseA(I1(), std::integral_constant<int, 0>(), SLOWC());
+        phaseA(I1(), std::integral_constant<int, 1>(), SLOWC());
+        phaseA(I1(), std::integral_constant<int, 2>(), SLOWC());
+        phaseA(I1(), std::integral_constant<int, 3>(), SLOWC());
+        __syncthreads();  // column maxima visible
+        scale_put();
       }
-      scB[b] = sc;
-      put(2 * wid, b, va[b], __builtin_amdgcn_ldexpf(1.f, sc));
     }
-    __syncthreads();      // chunk buffer complete
+    __syncthreads();      // chunk buffer complete (chunk 1: a no-op wait after the fast path)
     if (c == 0) KSTAMP(3);
     if (c == 1) KSUB(4);
     // ------------------------------------------------ phase B over the chunk's 16 K tiles

@@ -521,18 +521,27 @@ def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
         _close(a, b, rel=1e-5)
 
 
+@pytest.mark.parametrize('skew', [False, True])
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3])
-def test_fused_k128_vjp_matches_64px_kernel(block, B):
+def test_fused_k128_vjp_matches_64px_kernel(block, B, skew):
     """The 128-pixel K-chunked kernel (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
     256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net forward, the VJP, the chained log-det
     series (each term stages the previous term's taps, preact swish' and trace partial) and the Neumann vector
     (each term stages the accumulation w += c_k v_k), with the workspace and every CU's LDS NaN-poisoned before
     each call.  INF_OPT_FUSED_K128 = 2 forces the 128-pixel kernel at these small grids.  Tolerance: 1e-5 of
-    max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons."""
+    max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons.
+    skew: hidden units 256-511 of both hidden layers weighted 1000x (first conv's output rows, last conv's input
+    channels), so the second 256-row chunk's column maxima far exceed the first's and the 128-pixel kernel's chunk 1
+    leaves its fast put at chunk 0's scales for the exact-scale path."""
     arch = syn.CIFAR10
     m, _ = _model(arch, B)
     blk = imblocks(m)[block]
+    if skew:
+        convs = [mod for mod in blk.nnet_z if getattr(mod, 'weight', None) is not None]
+        with torch.no_grad():
+            convs[0].weight[256:] *= 1000.0
+            convs[-1].weight[:, 256:] *= 1000.0
     shape = blk.nnet_x[-1].weight.shape[0], 32 >> (block // 2), 32 >> (block // 2)
     torch.manual_seed(7)
     x = (torch.randn(B, *shape) * 0.5).to(DEV)
