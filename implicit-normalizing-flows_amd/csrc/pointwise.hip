@@ -388,20 +388,20 @@ __global__ __launch_bounds__(256) void broyden_p1(BroydenArgs a, int nchunk) {
   }
 }
 
-// Large d (CelebA-HQ: 192 chunks per sample): the chunk partials are summed once per sample into chunk 0's slot (the
-// same serial order the consumers used) instead of by every block of the sample; the consumers then read nsum = 1.
-// part[b][c][ld]: column col(j) = j < m1 ? j : off2 + j - m1, j < ncol
+// Large d (CelebA-HQ: 192 chunks per sample): the chunk partials are summed once per sample into chunk 0's slot instead
+// of by every block of the sample (each of 192 blocks re-summed all 192 partials); the consumers then read nsum = 1.
+// One wave per (sample, column): lanes over the chunks, a fixed shuffle tree (deterministic; a serial loop per column
+// took 42 us per call).  part[b][c][ld]: column col(j) = j < m1 ? j : off2 + j - m1, j < ncol
 __global__ __launch_bounds__(64) void br_sum_chunks(double* part, int nchunk, int ld, int m1, int off2, int ncol,
                                                     const int* active) {
-  const int b = blockIdx.x;
-  if (active && !active[b]) return;
-  for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
-    const int col = j < m1 ? j : off2 + (j - m1);
-    double* p = part + (long)b * nchunk * ld + col;
-    double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += p[(long)c * ld];
-    p[0] = s;
-  }
+  const int b = blockIdx.x, j = blockIdx.y, lane = threadIdx.x;
+  if (j >= ncol || (active && !active[b])) return;
+  const int col = j < m1 ? j : off2 + (j - m1);
+  double* p = part + (long)b * nchunk * ld + col;
+  double s = 0.0;
+  for (int c = lane; c < nchunk; c += 64) s += p[(long)c * ld];
+  s = wave_sum(s);
+  if (lane == 0) p[0] = s;
 }
 
 __global__ __launch_bounds__(256) void broyden_p2(BroydenArgs a, int nchunk, int nsum, double* part2) {
@@ -521,14 +521,14 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   if (a.m > 0) {
     hipLaunchKernelGGL(broyden_p1, grid, dim3(256), 0, s, a, nchunk);
     INF_CHECK_LAUNCH();
-    if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, a.part, nchunk, 2 * a.T, a.m, a.T, 2 * a.m, a.active);
+    if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, 2 * a.m), dim3(64), 0, s, a.part, nchunk, 2 * a.T, a.m, a.T, 2 * a.m, a.active);
   }
   hipLaunchKernelGGL(broyden_p2, grid, dim3(256), 0, s, a, nchunk, nsum, part2);
   INF_CHECK_LAUNCH();
-  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, part2, nchunk, 1, 1, 0, 1, a.active);
+  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, 1), dim3(64), 0, s, part2, nchunk, 1, 1, 0, 1, a.active);
   hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, nsum, part2, part3);
   INF_CHECK_LAUNCH();
-  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch), dim3(64), 0, s, part3, nchunk, a.T, a.ncols, 0, a.ncols, a.active);
+  if (pre && a.ncols > 0) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, a.ncols), dim3(64), 0, s, part3, nchunk, a.T, a.ncols, 0, a.ncols, a.active);
   hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, nsum, part3);
   INF_CHECK_LAUNCH();
   return INF_OK;
