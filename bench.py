@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Throughput of the implicit-flow density-evaluation hot path on MI355X.
 
-Workload (BASELINE.json metric, config C3/C4): CIFAR10 3x32x32 implicit flow of run_cifar10.sh
+Workload (BASELINE.json metric, config C3): CIFAR10 3x32x32 implicit flow of run_cifar10.sh
 (3 scales x 2 imBlocks, idim 512, swish, kernels 3-1-3, coeff 0.9, preact, actnorm, logit init),
 model.eval(): per imBlock a Broyden root solve + two power-series Hutchinson log-dets with
 20 + Poisson(2) terms, then bits/dim.  One step = one batch of `--batch` images per GPU through
@@ -9,8 +9,16 @@ the whole model; inputs are resident in HBM before the timed region.  Weights: d
 random init of that architecture (lib/synthetic.py); data: synthetic dequantised images.
 Probes: device RNG by default (`--probes reference` replays the reference's CPU RNG stream).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU)
+Other BASELINE.json configs (--config):
+  cifar10_c4   C4: the global batch of 2048 sharded over the ranks (2048 / N per GPU; strong scaling)
+  power        C2: POWER tabular (d = 6, batch 10 000, 20 imBlocks, 6-128x4-6 sin, exact 6x6 log-det in eval)
+  celebahq256  C5: CelebA-HQ 256 (5 bits, 4 scales), batch 4 per GPU
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config C] [--global-batch G]
+
+`--gpus N` (N > 1) without a torch.distributed launcher starts N rank processes (torch.distributed.run, one rank
+per GPU, RCCL) before anything touches the GPU and exits with their status; with fewer than N devices the ranks
+share them over gloo (a rehearsal).  Under torch.distributed.run (WORLD_SIZE set) each process is one rank.
 
 Prints one JSON line on rank 0 (metric, value = samples/s over all ranks, roofline of the
 dominant kernel measured live with HIP events, cpu_baseline = the oracle on the host cores).
@@ -20,6 +28,8 @@ import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,13 +44,23 @@ import torch  # noqa: E402
 
 from lib import _hip, distributed as dd, synthetic as syn  # noqa: E402
 from lib.configs import build_flow, imblocks, restore_engine_options, set_engine_option  # noqa: E402
-from lib.density import image_bits_per_dim_graph, image_logpx  # noqa: E402
+from lib.density import image_bits_per_dim_graph, image_logpx, tabular_logpx  # noqa: E402
 from lib.layers import set_probe_mode, set_probe_shard  # noqa: E402
 
 METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs are labelled alike
     'cifar10': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 density eval at 1/8 GPU',
+    'cifar10_c4': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 density eval at 1/8 GPU',
     'cifar10_small': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 (idim 64) density eval',
     'celebahq256': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CelebA-HQ 256 density eval',
+    'power': 'samples/sec (whole node) + nats \u0394 vs ref, POWER tabular density eval',
+}
+# --config -> (lib/synthetic.py architecture, per-GPU batch, global batch): BASELINE.json configs[1..4]
+BENCH_CONFIGS = {
+    'cifar10': ('cifar10', 64, None),          # C3 (and the per-GPU batch of the weak-scaling runs)
+    'cifar10_c4': ('cifar10', None, 2048),     # C4: 2048 over the ranks
+    'cifar10_small': ('cifar10_small', 64, None),
+    'celebahq256': ('celebahq256', 4, None),   # C5
+    'power': ('power', 10000, None),           # C2
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA peak (1024 flop/clk/SIMD x 1024 SIMDs x 2.4 GHz)
@@ -81,12 +101,16 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--batch', type=int, default=64, help='images per GPU')
-    ap.add_argument('--config', default='cifar10', choices=['cifar10', 'cifar10_small', 'celebahq256'])
+    ap.add_argument('--batch', type=int, default=None, help='samples per GPU (default: the config\'s)')
+    ap.add_argument('--global-batch', type=int, default=None,
+                    help='samples over all ranks (per-GPU batch = G / N); cifar10_c4 defaults to 2048')
+    ap.add_argument('--config', default='cifar10', choices=sorted(BENCH_CONFIGS))
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
     ap.add_argument('--cpu-batch', type=int, default=8,
-                    help='images per timed CPU-baseline batch (1 warm-up batch of half that, then the median of 3)')
+                    help='images per timed CPU-baseline batch (1 warm-up batch of half that, then the median of 3); '
+                         'per-sample CPU time is batch-independent from 8 to 64 images '
+                         '(profiles/r04/cpu_baseline_batch.json); tabular configs time the bench batch itself')
     ap.add_argument('--train-step', default='full', choices=['full', 'fwdbwd'],
                     help='train mode: full = forward + backward + clip_grad_norm_(1) + Adam + update_lipschitz + '
                          'EMA (train_img.py:637-658); fwdbwd = forward + backward only')
@@ -96,39 +120,97 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads():
+    """`nproc` of the host (BASELINE.md:36: the CPU baseline runs on N = nproc threads).  GNU nproc honours the
+    process's CPU affinity and OMP_NUM_THREADS, i.e. the CPU share the job actually has; os.cpu_count() is the
+    whole machine's count and is reported beside it."""
+    try:
+        n = int(subprocess.run(['nproc'], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        n = len(os.sched_getaffinity(0))
+    return max(1, n)
+
+
 def cpu_baseline(arch, sd, model, device, nimg):
     """Oracle (CPU restatement, torch fp32, autograd VJPs) timed as BASELINE.md's CPU-baseline plan prescribes --
-    one warm-up batch, then the median of 3 batches -- on batches of `nimg` images (bounded: B=64 batches would take
-    minutes of CPU per batch); also the GPU path on the last batch with the reference RNG replay ->
-    |bpd_gpu - bpd_oracle|."""
+    N = nproc threads, one warm-up batch, then the median of 3 batches.  Images: batches of `nimg` (per-sample
+    CPU time does not depend on the batch from 8 to 64 images, profiles/r04/cpu_baseline_batch.json; a B = 64
+    batch takes minutes of CPU).  Tabular: the bench batch itself.  Also runs the GPU path on the last batch with
+    the reference RNG replay -> |loss_gpu - loss_oracle| (bits/dim or nats)."""
     from oracle import inflow_oracle as orc
-    cores = max(1, min(int(os.environ.get('OMP_NUM_THREADS', '16')), os.cpu_count() or 1))
+    cores = host_threads()
     torch.set_num_threads(cores)
-    flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
-    xw = syn.image_batch(max(1, nimg // 2), arch['input_size'], arch['nvals'], seed=776)
+    image = arch['kind'] == 'conv'
+    if image:
+        flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
+        batch = lambda n, seed: syn.image_batch(n, arch['input_size'], arch['nvals'], seed=seed)
+        run = lambda xb: orc.image_bits_per_dim(flow, xb, arch['nvals'])
+        warm_n = max(1, nimg // 2)
+    else:
+        flow = orc.build(arch, sd, syn.fc_flow_layout(arch))
+        batch = lambda n, seed: syn.tabular_batch(n, arch['d'], seed=seed)
+        run = lambda xb: orc.tabular_nats(flow, xb)
+        warm_n = nimg
     np.random.seed(10)
     torch.manual_seed(10)
-    orc.image_bits_per_dim(flow, xw, arch['nvals'])            # warm-up batch (untimed)
+    run(batch(warm_n, 776))                                    # warm-up batch (untimed)
     times = []
     for r in range(3):
-        x = syn.image_batch(nimg, arch['input_size'], arch['nvals'], seed=777 + r)
+        x = batch(nimg, 777 + r)
         np.random.seed(11 + r)
         torch.manual_seed(11 + r)
         t0 = time.perf_counter()
-        ref_bpd, _, _ = orc.image_bits_per_dim(flow, x, arch['nvals'])
+        ref_loss, _, _ = run(x)
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times))
     set_probe_mode('reference')
     np.random.seed(11 + 2)
     torch.manual_seed(11 + 2)
-    gpu_bpd, _, _ = image_logpx(model, x.to(device), arch['nvals'])
+    if image:
+        gpu_loss, _, _ = image_logpx(model, x.to(device), arch['nvals'])
+    else:
+        gpu_loss, _, _ = tabular_logpx(model, x.to(device))
     torch.cuda.synchronize()
     set_probe_mode('device', seed=12345)
-    return ({'value': nimg / dt, 'unit': 'samples/s', 'cores': cores, 'kind': 'port',
-             'sample': 'oracle/inflow_oracle.py (torch fp32 CPU, %d threads) on the full run_cifar10.sh model: one '
-                       'warm-up batch of %d images, then the median of 3 batches of %d CIFAR-shaped images '
-                       '(%.1f / %.1f / %.1f s)' % (cores, max(1, nimg // 2), nimg, *times)},
-            abs(float(gpu_bpd) - float(ref_bpd)), float(ref_bpd))
+    what = ('the full run_cifar10.sh model' if arch.get('idim') == 512 and arch['input_size'] == (3, 32, 32)
+            else 'the bench model')
+    return ({'value': nimg / dt, 'unit': 'samples/s', 'cores': cores, 'nproc': cores, 'threads': cores,
+             'os_cpu_count': os.cpu_count(), 'kind': 'port',
+             'sample': 'oracle/inflow_oracle.py (torch fp32 CPU, torch.set_num_threads(nproc = %d)) on %s: one '
+                       'warm-up batch of %d, then the median of 3 batches of %d %s (%.1f / %.1f / %.1f s)'
+                       % (cores, what, warm_n, nimg, 'images' if image else 'rows', *times)},
+            abs(float(gpu_loss) - float(ref_loss)), float(ref_loss))
+
+
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: one rank per GPU through torch.distributed.run (started before this process
+    touches the GPU; counting devices does not initialise it), returning the ranks' exit status.  RCCL when there
+    are N devices; a gloo rehearsal (ranks sharing the devices) otherwise."""
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    if torch.cuda.device_count() < args.gpus:
+        env.setdefault('INFLOW_DIST_BACKEND', 'gloo')
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args.gpus),
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def per_gpu_batch(args, world):
+    arch_name, batch, global_batch = BENCH_CONFIGS[args.config]
+    if args.batch is not None and args.global_batch is not None:
+        raise SystemExit('--batch and --global-batch are exclusive')
+    if args.batch is not None:
+        return args.batch, None
+    gb = args.global_batch if args.global_batch is not None else global_batch
+    if gb is None:
+        return batch, None
+    if gb % world:
+        raise SystemExit('global batch %d does not split over %d ranks' % (gb, world))
+    return gb // world, gb
 
 
 def main():
@@ -136,16 +218,25 @@ def main():
     rank, world = dd.init_from_env()
     device = torch.device('cuda', dd.local_device_index())
     torch.cuda.set_device(device)
-    arch = syn.CONFIGS[args.config]
-    B = args.batch
-    sd = syn.make_state_dict(arch, 0, power_iters=30 if args.config != 'celebahq256' else 5)
+    arch_name = BENCH_CONFIGS[args.config][0]
+    arch = syn.CONFIGS[arch_name]
+    image = arch['kind'] == 'conv'
+    B, global_batch = per_gpu_batch(args, world)
+    sd = syn.make_state_dict(arch, 0, power_iters=30 if arch_name != 'celebahq256' else 5)
     model = build_flow(arch, B)
     model.load_state_dict(sd, strict=True)
     model = model.to(device).eval()
     nsteps = args.warmup + args.steps
-    xs = torch.stack([syn.image_batch(B, arch['input_size'], arch['nvals'], seed=1000 * rank + i)
-                      for i in range(min(nsteps, 4))]).to(device)
-    ndim = int(np.prod(arch['input_size']))
+    if image:
+        xs = torch.stack([syn.image_batch(B, arch['input_size'], arch['nvals'], seed=1000 * rank + i)
+                          for i in range(min(nsteps, 4))]).to(device)
+        ndim = int(np.prod(arch['input_size']))
+    else:
+        if args.mode == 'train':
+            raise SystemExit('--mode train runs the image configs')
+        xs = torch.stack([syn.tabular_batch(B, arch['d'], seed=1000 * rank + i)
+                          for i in range(min(nsteps, 4))]).to(device)
+        ndim = arch['d']
     # probes in the global reference order, each rank keeping its rows: the same probes per sample
     # as a single-process run over the world * B batch
     set_probe_mode(args.probes, seed=12345)
@@ -177,9 +268,12 @@ def main():
                 update_lipschitz(model)
                 ema.apply()
             return bpd.detach()
-        _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
+        if image:
+            _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
+        else:
+            _, logpx, _ = tabular_logpx(model, xs[i % xs.shape[0]])
         s, n = dd.global_logpx_sum(logpx)      # the one collective per batch
-        return dd.bits_per_dim(s, n, ndim)
+        return dd.bits_per_dim(s, n, ndim) if image else -s / n
 
     for i in range(args.warmup):
         step(i)
@@ -224,7 +318,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            if (pmc.get('tag') == dom['tag'] and pmc.get('batch') == B and args.config == pmc.get('config', 'cifar10')
+            if (pmc.get('tag') == dom['tag'] and pmc.get('batch') == B and arch_name == pmc.get('config', 'cifar10')
                     and pmc.get('kernel_source_sha') == kernel_source_sha()):
                 traffic = pmc.get('hbm_bytes_per_launch')
                 traffic_src = 'profiles/pmc_dominant_kernel.json (%s)' % pmc.get('measured', '?')
@@ -237,6 +331,16 @@ def main():
     # fp32-equivalent peak of the arithmetic the dominant kernel issues: its algorithmic FLOPs over the time its
     # MFMA instructions take at their dense peak (engine prof peak_ms; frac = MFMA-pipe fraction)
     peak = dom['flops'] / (dom['peak_ms'] * 1e9) if dom.get('peak_ms') else FP32_MFMA_PEAK_TFLOPS
+    what = 'density eval' if args.mode == 'eval' else 'training step'
+    if args.config == 'power':
+        workload = ('power: POWER tabular implicit flow %s (run_tabular.sh arch: 20 imBlocks, 6-128x4-6 sin, '
+                    'coeff 0.99, exact 6x6 log-det), batch %d per GPU' % (what, B))
+    elif global_batch is not None:
+        workload = ('%s: CIFAR10 implicit flow %s (run_cifar10.sh arch), global batch %d sharded over %d GPU%s '
+                    '(%d per GPU)' % (args.config, what, global_batch, world, 's' if world > 1 else '', B))
+    else:
+        workload = '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU' % (
+            args.config, what, '' if args.config == 'cifar10' else ' variant', B)
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
         'samples/sec (whole node), %s training step (%s)' % (
@@ -244,16 +348,17 @@ def main():
             if args.train_step == 'full' else 'forward + backward'),
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'scaling': 'strong' if global_batch is not None else 'weak', 'vs_baseline': None, 'dtype': 'f32',
         'mfma': MFMA_DESC[mm],
-        'data': 'synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
-                % 'x'.join(map(str, arch['input_size'])),
-        'config': {'workload': '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU'
-                               % (args.config, 'density eval' if args.mode == 'eval' else 'training step',
-                                  '' if args.config == 'cifar10' else ' variant', B),
+        'data': ('synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
+                 % 'x'.join(map(str, arch['input_size']))) if image else
+                ('synthetic standardised N(0, 1) rows (d = %d), deterministic random-init weights (lib/synthetic.py)'
+                 % arch['d']),
+        'config': {'workload': workload,
                    'global_batch': B * world, 'per_gpu_batch': B, 'parallelism': 'dp%d' % world,
+                   'dist_backend': (torch.distributed.get_backend() if world > 1 else None),
                    'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps},
-        'bits_per_dim': round(bpd, 6),
+        ('bits_per_dim' if image else 'nats'): round(bpd, 6),
         'roofline': {'bound': 'mfma', 'kernel': _hip.tag_name(dom['tag']), 'achieved': round(achieved, 2),
                      'peak': round(peak, 1), 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4),
                      'peak_basis': ('fp32-equivalent: algorithmic FLOPs / time of the issued MFMA instructions at '
@@ -276,10 +381,10 @@ def main():
                                     for s in stats], key=lambda r: -r['ms'])[:12]},
         'cpu_baseline': None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline and args.config != 'celebahq256' and args.mode == 'eval':
-        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch)
+    if rank == 0 and world == 1 and args.cpu_baseline and arch_name != 'celebahq256' and args.mode == 'eval':
+        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch if image else B)
         out['cpu_baseline'] = cb
-        out['bpd_delta_vs_oracle'] = delta
+        out['bpd_delta_vs_oracle' if image else 'nats_delta_vs_oracle'] = delta
         out['speedup_vs_cpu_baseline'] = round(value / cb['value'], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -288,4 +393,7 @@ def main():
 
 
 if __name__ == '__main__':
+    _args = parse()
+    if _args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(_args))
     main()

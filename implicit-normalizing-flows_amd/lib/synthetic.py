@@ -285,6 +285,61 @@ POWER_ITER_LAYERS = [   # (arch, key, kind, cin, cout, k, hw, n_iterations, pert
 ]
 
 
+# Broyden's protective break (broyden.py:169-172) and the Banach fallback it triggers (implicit_block.py:74-75,
+# 57-65,17-28), on a single fc imBlock over d = 6 (tests/golden/make_golden_edges.py prot_break_b6):
+#   nnet_x == 0 (zero weights and biases), so x_embed == x bit for bit;
+#   nnet_z(z) = W2 sin(2 pi W1 z) / (2 pi) with a nilpotent coupling chain z0 -> z1 -> z2 -> z3:
+#     f1 = C s(K z0), f2 = D s(z1), f3 = D s(z2), s(t) = sin(2 pi t) / (2 pi);
+#   x ~ 1e-9 N(0, 1) with eps_forward 1e-13.
+# Broyden's first step goes to z = -g(0) = -x, where |f1| ~ C / (2 pi) against an initial residual ~ |x|: the
+# residual grows by ~1e8 (> 1e6: prot_break, with two orders of margin).  The Banach iteration z <- x - f(z) then
+# settles one chain level per iteration and stops with an exactly-zero change after 3 iterations.  Samples whose
+# z0 is exactly 0 never see the K coupling: their (linear, tiny) solve converges in Broyden (per-sample mode keeps
+# their Broyden result).  J_f is nilpotent, so the exact log-dets are 0 up to rounding.
+PROT_BREAK = dict(d=6, hidden=8, K=1e9, C=6.0, D=0.9, coeff=1e12, eps_forward=1e-13, x_scale=1e-9,
+                  zero_rows=(1, 4), B=6)
+
+
+def prot_break_nets_state():
+    """State dict of the prot_break imBlock's nets (InducedNormLinear(6, 8), Sin, InducedNormLinear(8, 6)) and their
+    frozen copies; u / v are the exact top singular vectors (sigma = K and C, far below coeff: W_eff == W)."""
+    p = PROT_BREAK
+    d, h = p['d'], p['hidden']
+    W1 = np.zeros((h, d), np.float32)
+    W2 = np.zeros((d, h), np.float32)
+    W1[0, 0], W1[1, 1], W1[2, 2] = p['K'], 1.0, 1.0
+    W2[1, 0], W2[2, 1], W2[3, 2] = p['C'], p['D'], p['D']
+    e = lambda n, i: _t(np.eye(n, dtype=np.float32)[i])
+    sd = OrderedDict()
+    sd['lamb'] = torch.tensor(2.0)
+    sd['last_n_samples'] = torch.zeros(1)
+    sd['last_firmom'] = torch.zeros(1)
+    sd['last_secmom'] = torch.zeros(1)
+    for net in ('nnet_x', 'nnet_z'):
+        zero = net == 'nnet_x'
+        sd[net + '.0.weight'] = _t(np.zeros_like(W1) if zero else W1)
+        sd[net + '.0.bias'] = torch.zeros(h)
+        sd[net + '.0.scale'] = torch.tensor(0. if zero else float(p['K']))
+        sd[net + '.0.u'], sd[net + '.0.v'] = e(h, 0), e(d, 0)
+        sd[net + '.2.weight'] = _t(np.zeros_like(W2) if zero else W2)
+        sd[net + '.2.bias'] = torch.zeros(d)
+        sd[net + '.2.scale'] = torch.tensor(0. if zero else float(p['C']))
+        sd[net + '.2.u'], sd[net + '.2.v'] = e(d, 1), e(h, 0)
+    for k in list(sd.keys()):
+        if k.startswith('nnet_'):
+            sd[k.replace('nnet_x.', 'nnet_x_copy.', 1).replace('nnet_z.', 'nnet_z_copy.', 1)] = sd[k].clone()
+    return sd
+
+
+def prot_break_batch(seed=5):
+    p = PROT_BREAK
+    g = torch.Generator().manual_seed(int(seed))
+    x = torch.randn(p['B'], p['d'], generator=g) * p['x_scale']
+    for r in p['zero_rows']:
+        x[r, 0] = 0.
+    return x
+
+
 def perturbed_weight(sd, key, seed=1, scale=0.05):
     """sd[key + '.weight'] moved off its converged u / v (as after an optimiser step): W + scale * std(W) * N(0, 1),
     deterministic (numpy PCG64 keyed like the weights).  Power-iteration fixtures start from it."""

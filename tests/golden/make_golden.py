@@ -125,7 +125,9 @@ def fc_model(arch):
     return layers.SequentialFlow(blocks)
 
 
-def run_case(name, arch, x, seed, weight_seed=0, train=False, power_iters=30):
+def run_case(name, arch, x, seed, weight_seed=0, train=False, power_iters=30, x_seed=None):
+    """x_seed: x is syn.image_batch(B, seed=x_seed) and the fixture keeps only that seed and x's per-sample sums
+    (large batches), not x itself."""
     torch.manual_seed(1234)
     model = conv_model(arch, x.shape[0]) if arch['kind'] == 'conv' else fc_model(arch)
     with torch.no_grad():
@@ -157,6 +159,11 @@ def run_case(name, arch, x, seed, weight_seed=0, train=False, power_iters=30):
                logpx=logpx.detach().view(-1).numpy().astype(np.float64),
                z=z.detach().view(x.shape[0], -1).numpy().astype(np.float32), seconds=np.float64(dt),
                nblocks=np.int64(len(REC)), power_iters=np.int64(power_iters))
+    if x_seed is not None:
+        del out['x']
+        out['x_seed'] = np.int64(x_seed)
+        out['xsum'] = x.detach().reshape(x.shape[0], -1).double().sum(1).numpy()
+        out['z'] = out['z'].astype(np.float64).sum(1)     # per-sample sums of the flow output
     for i, r in enumerate(REC):
         for k, v in r.items():
             if k == 'z' and x.shape[0] * v[0].size >= 100000:    # large batches: per-sample sums only
@@ -184,6 +191,9 @@ CASES = {
     'cifar_full_b8': lambda: run_case('cifar_full_b8', syn.CIFAR10, syn.image_batch(8, seed=5), seed=11),
     # the headline bench configuration (BASELINE.json configs[2]: run_cifar10.sh, batch 64)
     'cifar_full_b64': lambda: run_case('cifar_full_b64', syn.CIFAR10, syn.image_batch(64, seed=0), seed=0),
+    # BASELINE.json configs[3]'s per-GPU shard: 2048 images over 8 GPUs = 256 per rank (x regenerated from its seed)
+    'cifar_full_b256': lambda: run_case('cifar_full_b256', syn.CIFAR10, syn.image_batch(256, seed=21), seed=21,
+                                        x_seed=21),
     # BASELINE.json configs[4]: CelebA-HQ 256 (5 bits, 4 scales), one image; weights with 5 power iterations as bench.py
     'celebahq256_b1': lambda: run_case('celebahq256_b1', syn.CELEBAHQ256,
                                        syn.image_batch(1, (3, 256, 256), 32, seed=2), seed=4, power_iters=5),

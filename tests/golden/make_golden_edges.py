@@ -337,7 +337,95 @@ def per_sample_broyden(orig):
     return broyden
 
 
+# ---- a3: protective break -> Banach fallback ------------------------------------------------------------
+def _prot_break_block():
+    p = syn.PROT_BREAK
+    lin = lambda a, b: base_layers.InducedNormLinear(a, b, coeff=p['coeff'], n_iterations=None, atol=1e-3, rtol=1e-3,
+                                                     domain=2, codomain=2)
+    net = lambda: torch.nn.Sequential(lin(p['d'], p['hidden']), base_layers.Sin(), lin(p['hidden'], p['d']))
+    blk = layers.imBlock(net(), net(), n_dist='geometric', n_power_series=None, exact_trace=False, brute_force=False,
+                         n_samples=1, n_exact_terms=2, neumann_grad=False, grad_in_forward=False,
+                         eps_forward=p['eps_forward'])
+    blk.load_state_dict(syn.prot_break_nets_state(), strict=True)
+    return blk.eval()
+
+
+def prot_break_case(seed=5):
+    """One fc imBlock (lib/synthetic.py PROT_BREAK) whose Broyden solve breaks at its first step: the batch
+    (broyden.py:169-172 -> implicit_block.py:74-75, find_fixed_point from z0 = x with eps_forward and 1000
+    iterations), and each sample as a batch of one (broyden_find_root per sample: only the samples whose own solve
+    breaks take the fixed point)."""
+    x = syn.prot_break_batch(seed)
+    B = x.shape[0]
+    counts = {'g': 0, 'fp': []}
+    orig_ffp = ib.find_fixed_point
+
+    def ffp(g, y, threshold=1000, eps=1e-5):
+        def gc(t):
+            counts['g'] += 1
+            return g(t)
+        counts['g'] = 0
+        r = orig_ffp(gc, y, threshold=threshold, eps=eps)
+        counts['fp'].append(counts['g'] - 1)           # g(y) first, then one g per loop iteration
+        return r
+    ib.find_fixed_point = ffp
+    out = dict(x=x.numpy(), seed=np.int64(seed))
+    orig_bfr = ib.RootFind.broyden_find_root
+    try:
+        for tag, per_sample in (('g', False), ('ps', True)):
+            blk = _prot_break_block()
+            counts['fp'] = []
+            stats = []
+
+            def bfr(nnet_z, nnet_x, z0, xx, *args):
+                if not per_sample:
+                    return orig_bfr(nnet_z, nnet_x, z0, xx, *args)
+                rows = []
+                for b in range(xx.shape[0]):
+                    n0 = len(counts['fp'])
+                    rows.append(orig_bfr(nnet_z, nnet_x, z0[b:b + 1], xx[b:b + 1], *args))
+                    if len(counts['fp']) == n0:
+                        counts['fp'].append(-1)              # this sample kept its Broyden result
+                return torch.cat(rows)
+            ib.RootFind.broyden_find_root = staticmethod(bfr)
+            prev = ib.broyden
+
+            def broyden(*a, **k):
+                r = prev(*a, **k)
+                stats.append(dict(nstep=r['nstep'], lowest_step=r['lowest_step'], prot_break=int(r['prot_break']),
+                                  trace=np.array(r['trace'])))
+                return r
+            ib.broyden = broyden
+            try:
+                with torch.no_grad():
+                    z, lp = blk(x, torch.zeros(B, 1))
+            finally:
+                ib.broyden = prev
+                ib.RootFind.broyden_find_root = orig_bfr
+            z, lp = z.detach(), lp.detach()
+            logpz = (-0.5 * np.log(2 * np.pi) - z.pow(2) / 2).sum(1, keepdim=True)
+            logpx = logpz + lp
+            out.update({tag + '_z': z.numpy().astype(np.float32), tag + '_logdet': (-lp).view(-1).numpy().astype(np.float64),
+                        tag + '_logpx': logpx.view(-1).numpy().astype(np.float64),
+                        tag + '_nats': np.float64(-logpx.mean().item()),
+                        tag + '_nstep': np.array([s['nstep'] for s in stats]),
+                        tag + '_lowest_step': np.array([s['lowest_step'] for s in stats]),
+                        tag + '_prot_break': np.array([s['prot_break'] for s in stats]),
+                        tag + '_fixed_point_iters': np.array(counts['fp'])})
+            for i, s in enumerate(stats):
+                out['%s_trace%d' % (tag, i)] = s['trace']
+            print('   %s: nstep=%s prot_break=%s fixed_point_iters=%s nats=%.8f' % (
+                tag, [s['nstep'] for s in stats], [s['prot_break'] for s in stats], counts['fp'],
+                -logpx.mean().item()))
+            for s in stats:
+                print('      trace', np.array2string(s['trace'], precision=3))
+    finally:
+        ib.find_fixed_point = orig_ffp
+    _save('prot_break_b6', out)
+
+
 CASES = {
+    'prot_break_b6': prot_break_case,
     'power_iter_layers': power_iter_layers,
     'inverse_small_b4': lambda: inverse_case('inverse_small_b4', syn.CIFAR10_SMALL, 4, 12),
     'inverse_full_b2': lambda: inverse_case('inverse_full_b2', syn.CIFAR10, 2, 13),

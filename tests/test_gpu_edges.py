@@ -20,7 +20,7 @@ import torch
 from lib import _hip, synthetic as syn
 from lib.configs import build_flow, imblocks
 from lib.density import image_logpx
-from lib.layers import RootFind, iResBlock, set_probe_mode
+from lib.layers import RootFind, iResBlock, imBlock, set_probe_mode
 from lib.layers.base import InducedNormConv2d, Sin, Swish, get_linear
 from lib.layers.base import lipschitz_ops as lo
 
@@ -209,3 +209,50 @@ def test_degenerate_broyden_update_matches_reference(golden_dir):
     assert z[0].abs().max().item() <= 1e-6
     np.testing.assert_allclose(z.cpu().numpy(), g['z'], rtol=0, atol=2e-4)
     np.testing.assert_allclose((-lp).view(-1).cpu().numpy(), g['logdet'], rtol=0, atol=2e-3)
+
+
+def _prot_break_block():
+    p = syn.PROT_BREAK
+    lin = lambda a, b: get_linear(a, b, coeff=p['coeff'], n_iterations=None, atol=1e-3, rtol=1e-3, domain=2,
+                                  codomain=2)
+    net = lambda: torch.nn.Sequential(lin(p['d'], p['hidden']), Sin(), lin(p['hidden'], p['d']))
+    blk = imBlock(net(), net(), n_dist='geometric', n_power_series=None, exact_trace=False, brute_force=False,
+                  n_samples=1, n_exact_terms=2, neumann_grad=False, grad_in_forward=False,
+                  eps_forward=p['eps_forward'])
+    blk.load_state_dict(syn.prot_break_nets_state(), strict=True)
+    return blk.to(DEV).eval()
+
+
+@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
+def test_protective_break_banach_fallback_matches_reference(golden_dir, convergence):
+    """Broyden's protective break (residual > 1e6 x the initial one, broyden.py:169-172) and the Banach fallback
+    it triggers (implicit_block.py:74-75 -> banach_find_root from z0 = x, eps_forward, 1000 iterations, :57-65,
+    17-28), against the reference on lib/synthetic.py's PROT_BREAK block (prot_break_b6): global rule -> the batch
+    breaks at step 1 and the whole batch takes the fixed point; per-sample rule -> each sample as a batch of one
+    (the samples with z0 == 0 keep their Broyden result).  prot_break and the fixed-point iteration count exact,
+    per-sample Broyden steps exact, z within 2e-5, per-sample log p within 2e-3 nats, nats within 1e-5."""
+    g = _golden(golden_dir, 'prot_break_b6')
+    tag = 'g' if convergence == 'global' else 'ps'
+    x = torch.from_numpy(g['x']).to(DEV)
+    torch.testing.assert_close(x.cpu(), syn.prot_break_batch(int(g['seed'])), rtol=0, atol=0)
+    B = x.shape[0]
+    blk = _prot_break_block()
+    blk.convergence = convergence
+    with torch.no_grad():
+        z, lp = blk(x, torch.zeros(B, 1, device=DEV))
+    torch.cuda.synchronize()
+    st = blk.last_broyden
+    assert st['prot_break'], st
+    fp_ref = g[tag + '_fixed_point_iters']
+    assert st['fixed_point_iters'] == int(fp_ref.max()), (st['fixed_point_iters'], fp_ref)
+    if convergence == 'global':
+        assert st['nstep'] == int(g['g_nstep'][0])
+    else:
+        assert st['sample_prot_break'] == [int(v) for v in g['ps_prot_break']], st
+        assert st['sample_nstep'] == [int(v) for v in g['ps_nstep']], st
+    zr = g[tag + '_z']
+    np.testing.assert_allclose(z.cpu().numpy(), zr, rtol=0, atol=2e-5 * max(1., float(np.abs(zr).max())))
+    logpz = (-0.5 * np.log(2 * np.pi) - z.double().pow(2) / 2).sum(1)
+    logpx = (logpz + lp.double().view(-1)).cpu().numpy()
+    np.testing.assert_allclose(logpx, g[tag + '_logpx'], rtol=0, atol=2e-3)
+    assert abs(-logpx.mean() - float(g[tag + '_nats'])) <= 1e-5

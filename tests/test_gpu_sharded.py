@@ -104,13 +104,18 @@ def _free_port():
     return port
 
 
-def test_two_rank_sharded_eval(tmp_path):
+@pytest.mark.parametrize('B,mode', [(8, 'per_sample'), (512, 'per_sample'), (512, 'global')])
+def test_two_rank_sharded_eval(tmp_path, B, mode):
     """Two ranks (child processes, gloo, both on cuda:0; the driver's 8-GPU run uses RCCL) evaluate the two halves
-    of a batch of 8 with per-sample convergence; each rank's rows and the all-reduced bits/dim match the
-    single-process run on the whole batch."""
+    of a batch against the single-process run on the whole batch.  B = 512: each rank holds C4's per-GPU shard
+    (BASELINE.json configs[3]: 2048 over 8 GPUs = 256 per rank).
+      per_sample: each rank's rows and per-sample Broyden steps equal the single-process ones (log p within 2e-4
+                  nats), the all-reduced bits/dim within 1e-6;
+      global:     each shard stops on its own batch norm (the reference's DataParallel chunks do the same),
+                  bits/dim within 1e-5, per-sample log p within 2e-3 nats."""
     arch = syn.CIFAR10
-    B, seed = 8, 3
-    set_convergence('per_sample')
+    seed = 3
+    set_convergence(mode)
     try:
         bpd, lp, st = _run(arch, syn.image_batch(B, seed=seed), seed)
     finally:
@@ -121,14 +126,21 @@ def test_two_rank_sharded_eval(tmp_path):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE='2', MASTER_ADDR='127.0.0.1',
                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, 'workers', 'shard_eval.py'), '--batch',
-                                       str(B), '--seed', str(seed), '--out', str(tmp_path / ('r%d.json' % r))],
-                                      env=env))
+                                       str(B), '--seed', str(seed), '--convergence', mode,
+                                       '--out', str(tmp_path / ('r%d.json' % r))], env=env))
     codes = [p.wait(timeout=300) for p in procs]
     assert codes == [0, 0], codes
     res = [json.load(open(tmp_path / ('r%d.json' % r))) for r in range(2)]
     for r in res:
         assert r['n'] == B
-        assert abs(r['bpd'] - bpd) <= 1e-6, (r['bpd'], bpd)
-        np.testing.assert_allclose(np.array(r['logpx']), lp[r['lo']:r['hi']], rtol=0, atol=2e-4)
-        for i, s in enumerate(st):
-            assert r['sample_nstep'][i] == s['sample_nstep'][r['lo']:r['hi']]
+        assert r['hi'] - r['lo'] == B // 2
+        print('%s B=%d rank %d: |dbpd| %.3g, max |dlogp| %.3g' % (mode, B, r['rank'], abs(r['bpd'] - bpd), np.abs(
+            np.array(r['logpx']) - lp[r['lo']:r['hi']]).max()))
+        if mode == 'per_sample':
+            assert abs(r['bpd'] - bpd) <= 1e-6, (r['bpd'], bpd)
+            np.testing.assert_allclose(np.array(r['logpx']), lp[r['lo']:r['hi']], rtol=0, atol=2e-4)
+            for i, s in enumerate(st):
+                assert r['sample_nstep'][i] == s['sample_nstep'][r['lo']:r['hi']]
+        else:
+            assert abs(r['bpd'] - bpd) <= 1e-5, (r['bpd'], bpd)
+            np.testing.assert_allclose(np.array(r['logpx']), lp[r['lo']:r['hi']], rtol=4e-7, atol=2e-3)

@@ -52,3 +52,32 @@ def test_oracle_matches_reference(golden_dir, name, arch, train):
     assert abs(loss - float(g['loss'])) < 1e-5
     np.testing.assert_allclose(logpx, g['logpx'], rtol=0, atol=2e-3)
     np.testing.assert_allclose(z.reshape(z.shape[0], -1), g['z'], rtol=0, atol=2e-4)
+
+
+def test_oracle_protective_break_matches_reference(golden_dir):
+    """The oracle's root_find (broyden -> prot_break -> find_fixed_point) on the PROT_BREAK block against the
+    reference (prot_break_b6): batch-wide, and each sample as a batch of one."""
+    path = os.path.join(golden_dir, 'prot_break_b6.npz')
+    if not os.path.exists(path):
+        pytest.skip('fixture prot_break_b6 not generated')
+    g = np.load(path)
+    p = syn.PROT_BREAK
+    sd = syn.prot_break_nets_state()
+    layout = [('linear', p['d'], p['hidden']), ('sin',), ('linear', p['hidden'], p['d'])]
+    fx, fz = (orc.make_net(sd, n, layout, p['coeff']) for n in ('nnet_x', 'nnet_z'))
+    x = torch.from_numpy(g['x'])
+    torch.testing.assert_close(x, syn.prot_break_batch(int(g['seed'])), rtol=0, atol=0)
+    with torch.no_grad():
+        zs, info = orc.root_find(fz, fx, x, x, p['eps_forward'], 30)
+        assert info['prot_break'] and info['nstep'] == int(g['g_nstep'][0])
+        z = fx(x) - fz(zs) + x
+        np.testing.assert_allclose(z.numpy(), g['g_z'], rtol=0, atol=2e-5 * max(1., float(np.abs(g['g_z']).max())))
+        rows, breaks = [], []
+        for b in range(x.shape[0]):
+            zb, ib = orc.root_find(fz, fx, x[b:b + 1], x[b:b + 1], p['eps_forward'], 30)
+            rows.append(zb)
+            breaks.append(int(ib['prot_break']))
+            assert ib['nstep'] == int(g['ps_nstep'][b]), b
+        assert breaks == [int(v) for v in g['ps_prot_break']]
+        z = fx(x) - fz(torch.cat(rows)) + x
+        np.testing.assert_allclose(z.numpy(), g['ps_z'], rtol=0, atol=2e-5 * max(1., float(np.abs(g['ps_z']).max())))
