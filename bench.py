@@ -290,7 +290,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- live per-kernel timing (one extra step, outside the timed region) ----
-    # The timed steps run the overlapped eval schedule (inf_set_eval_overlap: x-branch series on a side stream);
+    # The timed steps run the overlapped eval schedule (INF_OPT_EVAL_OVERLAP: x-branch series on a side stream);
     # this step runs the sequential one, so each kernel's HIP-event duration is its own, not shared with a
     # concurrent launch (tools/profile_round.sh runs rocprofv3 with INFLOW_EVAL_OVERLAP=0 to match).
     steps_info = [b.last_broyden['nstep'] for b in imblocks(model)]

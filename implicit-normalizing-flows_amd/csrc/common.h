@@ -107,6 +107,12 @@ __device__ __forceinline__ T block_sum(T v, T* scratch /* >= 16 */) {
 // lane as 8 consecutive v_mfma_f32_32x32x2_f32 steps (lane l: row/column l&31, k = 8 (l>>5) + 0..7), so
 // the fragment-major layouts carry over unchanged: 6 bf16 MFMAs (32 cycles each) replace 8 fp32 ones
 // (64 cycles each).
+// Phase stamps of the fused kernels (s_memtime at phase boundaries, fused313.hip timing_report): 0 in the product
+// build; tools/build_alt_k128.py "stamps" compiles a separate library with 1.
+#ifndef INFLOW_PHASE_STAMPS
+#define INFLOW_PHASE_STAMPS 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -115,21 +121,11 @@ __device__ __forceinline__ void split3(const float (&x)[8], u32x4& h, u32x4& m, 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const unsigned u0 = __float_as_uint(x[2 * j]), u1 = __float_as_uint(x[2 * j + 1]);
-#ifdef INFLOW_SPLIT_PK
-    const f32x2 xv = {x[2 * j], x[2 * j + 1]};
-    const f32x2 hv = {__uint_as_float(u0 & 0xffff0000u), __uint_as_float(u1 & 0xffff0000u)};
-    const f32x2 r = xv - hv;                                  // v_pk_add_f32 (exact)
-    const unsigned v0 = __float_as_uint(r.x), v1 = __float_as_uint(r.y);
-    const f32x2 mv = {__uint_as_float(v0 & 0xffff0000u), __uint_as_float(v1 & 0xffff0000u)};
-    const f32x2 sl = r - mv;                                  // exact, <= 8 significant bits
-    const float s0 = sl.x, s1 = sl.y;
-#else
     const float r0 = x[2 * j] - __uint_as_float(u0 & 0xffff0000u);       // exact
     const float r1 = x[2 * j + 1] - __uint_as_float(u1 & 0xffff0000u);
     const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
     const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);             // exact, <= 8 significant bits
     const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
-#endif
     h[j] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
     m[j] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
     l[j] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);

@@ -113,6 +113,7 @@ struct InfNet {
   int k128 = 1;            // INF_OPT_FUSED_K128
   int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
+  int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
 };
 
 namespace {
@@ -270,6 +271,7 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.W = n->W;
   f.seg = n->W < 64 ? n->W : 64;
   f.k128 = n->k128;
+  f.exact_scale = n->exact_scale;
   return f;
 }
 
@@ -643,7 +645,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     INF_TRY(sums(1, xp, fp, slot[1]));
   }
   int n_active = B;
-  INF_TRY(wait_sumsq(slot[0], B, ss, &n_active));
+  INF_TRY(wait_sumsq(slot[0], B, ss, per_sample ? &n_active : nullptr));
   const double init = sqrt(total(ss));
   double obj = init, lowest = init;
   lowest_ss = ss;
@@ -695,7 +697,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
       };
       const bool spec = allow && !likely_last;
       if (spec) INF_TRY(enqueue_next(nstep + 1));
-      INF_TRY(wait_sumsq(slot[ps_], B, ss, &n_active));
+      INF_TRY(wait_sumsq(slot[ps_], B, ss, per_sample ? &n_active : nullptr));
       nstep += 1;
       x = xp;
       prev_obj = obj;
@@ -1051,12 +1053,8 @@ static int layer_param_grads(InfNet* n, int l, const float* G_tan, const float* 
   float* dW = grad_out(gr->dW, l);
   if (dW) {
     const long mn = (long)w.cout * w.cin * w.ks * w.ks;
-    // the primal operand's swish once per element (INFLOW_WGRAD_PREACT=0: inside the wgrad loaders)
-    static const bool pre_act = [] {
-      const char* e = getenv("INFLOW_WGRAD_PREACT");
-      return !(e && e[0] == '0');
-    }();
-    if (pre_act && G_pri && X_pri_beta) {
+    // the primal operand's swish once per element, not inside every output tile's loader
+    if (G_pri && X_pri_beta) {
       INF_TRY(launch_swish_apply(X_pri, X_pri_beta, gb.act, (long)B * w.cin * n->P, s));
       X_pri = gb.act;
       X_pri_beta = nullptr;
@@ -1228,12 +1226,30 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     }
   }
   {
-    const char* e = getenv("INFLOW_FUSED_K128");            // default of INF_OPT_FUSED_K128
-    if (e && *e) n->k128 = std::min(std::max(atoi(e), 0), 2);
-    e = getenv("INFLOW_EVAL_OVERLAP");                      // default of INF_OPT_EVAL_OVERLAP
-    if (e && *e) n->eval_overlap = e[0] == '1' ? 1 : 0;
-    e = getenv("INFLOW_CONVERGENCE");                       // default of INF_OPT_CONVERGENCE
-    if (e && *e) n->convergence = !strcmp(e, "per_sample") ? INF_CONV_PER_SAMPLE : INF_CONV_GLOBAL;
+    // defaults of the per-net options; an unrecognised value fails inf_net_create (as INFLOW_MFMA does) rather
+    // than silently selecting another rule
+    struct EnvOpt { const char* name; int* slot; const char* const* values; int n; };
+    static const char* const k128_v[] = {"0", "1", "2"};
+    static const char* const bin_v[] = {"0", "1"};
+    static const char* const conv_v[] = {"global", "per_sample"};
+    const EnvOpt opts[] = {{"INFLOW_FUSED_K128", &n->k128, k128_v, 3},
+                           {"INFLOW_EVAL_OVERLAP", &n->eval_overlap, bin_v, 2},
+                           {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2}};
+    for (const EnvOpt& o : opts) {
+      const char* e = getenv(o.name);
+      if (!e || !*e) continue;
+      int v = -1;
+      for (int i = 0; i < o.n; ++i)
+        if (!strcmp(e, o.values[i])) v = i;
+      if (v < 0) {
+        fprintf(stderr, "libinflow: %s=%s is not one of", o.name, e);
+        for (int i = 0; i < o.n; ++i) fprintf(stderr, " %s", o.values[i]);
+        fprintf(stderr, "\n");
+        delete n;
+        return INF_ERR_INVALID;
+      }
+      *o.slot = v;
+    }
   }
   // sigma scratch: one partial per 256 output elements of the largest conv (or per channel-split block)
   size_t sc = SIGMA_MAX_PARTS + 64;
@@ -1613,7 +1629,7 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
   Bufs bfa, bfb, bfc;
   carve(nx, B, T, w0, half, bfa);
   carve(nz, B, 1, w0 + half, zneed, bfb);
-  // Overlapped schedule (default; inf_set_eval_overlap / INFLOW_EVAL_OVERLAP=0 turn it off; needs workspace for a
+  // Overlapped schedule (default; inf_net_set_option(INF_OPT_EVAL_OVERLAP, 0) or INFLOW_EVAL_OVERLAP=0 at create turn it off; needs workspace for a
   // third region): the x-branch series depends only on x, so it runs on a side stream while this stream does the
   // root solve (sync-bound, and short of work at the 8x8 scale) and then the z-branch series; the two streams join
   // before returning.  Concurrent series launches also desynchronise the CUs' d1/d2 bursts (every 1-WG/CU tile
@@ -2122,6 +2138,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_FUSED_K128: slot = &n->k128; hi = 2; break;
     case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
+    case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;
     default: return -INF_ERR_INVALID;
   }
   if (value < lo || value > hi) return -INF_ERR_INVALID;
@@ -2136,6 +2153,7 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_FUSED_K128: return n->k128;
     case INF_OPT_EVAL_OVERLAP: return n->eval_overlap;
     case INF_OPT_CONVERGENCE: return n->convergence;
+    case INF_OPT_K128_EXACT_SCALE: return n->exact_scale;
     default: return -INF_ERR_INVALID;
   }
 }

@@ -56,7 +56,7 @@ constexpr int TSLOTS = 32;
 #endif
 #ifndef PB_DEPTH
 #define PB_DEPTH 2   // phase-B weight prefetch ring (K tiles); 2 = ping-pong
-#endif   // INFLOW_FUSED_TIMING stamps per workgroup
+#endif   // INFLOW_PHASE_STAMPS stamps per workgroup
 
 __device__ __forceinline__ void load_frag8(const float* base, float* o) {
   const f32x4 v0 = *reinterpret_cast<const f32x4*>(base);
@@ -110,20 +110,20 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
 #define STAMP(i_)                                                                            \
   do {                                                                                       \
-    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
+    if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
   // per-wave stamps (lane 0 of every wave): slot 8 + w at its phase-B end, 16 + w once its epilogue-B
   // multiplier has arrived
 #define WSTAMP(base_)                                                                         \
   do {                                                                                       \
-    if (pr.tbuf && (threadIdx.x & 63) == 0) {                                                \
+    if (INFLOW_PHASE_STAMPS && pr.tbuf && (threadIdx.x & 63) == 0) {                                                \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
       pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + (threadIdx.x >> 6)] = t_;                \
       if (NW == 4) pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + 4 + (threadIdx.x >> 6)] = t_; \
     }                                                                                        \
   } while (0)
   STAMP(0);
-  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
+  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int P = a.H * a.W;
@@ -161,8 +161,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   const float* in = a.in + (long)img * a.C * P;
   const float pre_sp = a.pre_beta ? softplus_f(ldc(a.pre_beta)) : 0.f;
   double dacc = 0.0;
-  if (pr.dbg & 8) {
-  } else if (a.in_taps) {
+  if (a.in_taps) {
     const float* ytap = a.in_taps + (long)img * a.M3 * P;
     const float* mx = a.vmul_x ? a.vmul_x + (long)img * a.C * P : nullptr;
     const float* ep = a.dot_eps ? a.dot_eps + (long)img * a.C * P : nullptr;
@@ -733,7 +732,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           if constexpr (MODE == MODE_VJP) acc[m][b][r] = acc[m][b][r] * dmul[m][b][r];
           else acc[m][b][r] = swish_fast_f(acc[m][b][r] + a.b2[o], sp2);
         }
-    if (pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
+    if (INFLOW_PHASE_STAMPS && pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
       float s_ = 0.f;
 #pragma unroll
       for (int m = 0; m < TM; ++m)
@@ -789,7 +788,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     float* Y = a.Y + (long)img * a.M3 * P;
     // rounds of 32 jobs (4 per wave); wide nets (9C > 32*32 tap rows per round) take several rounds.
     // The split-K path only occurs with <= 8 jobs, i.e. in a single round.
-    const int nrounds = (pr.dbg & 4) ? 0 : (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 4 * NW - 1) / (4 * NW);   // half-LDS: 1 (variant_fits)
+    const int nrounds = (F_LDS_FLOATS == LDS_HALF) ? 1 : (njobs + 4 * NW - 1) / (4 * NW);   // half-LDS: 1 (variant_fits)
     for (int round = 0; round < nrounds; ++round) {
     const int jbase = round * 4 * NW;
     f32x16 cacc[4];
@@ -987,7 +986,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }   // rounds
   }
   STAMP(7);
-  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
+  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
 #undef STAMP
 #undef WSTAMP
 }
@@ -1000,12 +999,6 @@ __global__ __launch_bounds__(512) void net313_kernel(Net313Pair pr) {
 template <int TM, int MODE, int SPL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void net313_kernel_h(Net313Pair pr) {
   net313_body<TM, MODE, 32, LDS_HALF, SPL>(pr);
-}
-// one wave per SIMD (4 waves x 4 row blocks): the whole register file per wave, so one wave's own
-// instruction stream overlaps its operand split with its MFMAs
-template <int TM, int MODE, int SPL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void net313_kernel_q(Net313Pair pr) {
-  net313_body<2 * TM, MODE, 64, LDS_FULL, SPL, 4>(pr);
 }
 template <int TM, int MODE, int SPL>
 __global__ __launch_bounds__(512) void net313_kernel_w(Net313Pair pr) {
@@ -1035,7 +1028,7 @@ int net313_supported(int hid, int C, int H, int W) {
 
 // Launch one or two nets (same shape) as one grid.  The 64-pixel tile is used unless the grid would
 // leave CUs idle (fewer than 256 workgroups), then 32-pixel tiles.
-// ---- INFLOW_FUSED_TIMING (development): per-phase s_memtime deltas of wave 0, averaged per kernel
+// ---- INFLOW_PHASE_STAMPS builds (development, tools/build_alt_k128.py stamps): per-phase s_memtime deltas of wave 0, averaged per kernel
 struct TimingAcc {
   double sum[7] = {0, 0, 0, 0, 0, 0, 0};
   double bmin = 0, bmax = 0, dmax = 0;   // per-wave phase-B ends / multiplier arrivals, relative to stamp 3
@@ -1114,10 +1107,6 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const Net313Args& a0 = args[0];
   if (!net313_supported(hid, a0.C, a0.H, a0.W) || nnets < 1 || nnets > 2) return INF_ERR_UNSUPPORTED;
   const int P = a0.H * a0.W;
-  static const int force_bn = [] {
-    const char* e = getenv("INFLOW_FUSED_BN");            // tuning knob: 32 / 64 (default: auto)
-    return e ? atoi(e) : 0;
-  }();
   // 64-pixel tiles unless the grid would leave CUs idle; then 32-pixel tiles two per CU; the wide
   // variant when neither fits
   const bool f64 = variant_fits(hid, a0.C, a0.H, a0.W, V64), fh = variant_fits(hid, a0.C, a0.H, a0.W, VHALF);
@@ -1126,13 +1115,6 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // at most one 32-pixel workgroup per CU anyway: the full-LDS variant (256 VGPRs, deeper operand
   // prefetch, paired phase-C jobs) beats the two-per-CU one (8x8 scale at B=64: 96 vs 102 us per term)
   if (var == VHALF && layout_nets * a0.B * (P / 32) <= 256 && variant_fits(hid, a0.C, a0.H, a0.W, VWIDE)) var = VWIDE;
-  if (force_bn == 64 && f64) var = V64;
-  if (force_bn == 32 && fh) var = VHALF;
-  static const int force_var = [] {
-    const char* e = getenv("INFLOW_FUSED_VARIANT");       // tuning knob: 0 64-px, 1 _h, 2 _w
-    return e ? atoi(e) : -1;
-  }();
-  if (force_var >= 0 && variant_fits(hid, a0.C, a0.H, a0.W, force_var)) var = force_var;
   const int bn = var == V64 ? 64 : 32;
   Net313Pair pr;
   pr.a[0] = args[0];
@@ -1143,39 +1125,19 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // VJP / EVAL variant policy (per net, INF_OPT_FUSED_K128): 0 the 64-pixel kernel only, 1 the 128-pixel
   // K-chunked kernel where its grid still covers every CU (default), 2 wherever it fits (tests)
   const int k128_pol = a0.k128;
-  const bool k128 = k128_pol && H3_AC && h3_args && var == V64 && force_bn == 0 &&
-                    force_var < 0 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
+  const bool k128 = k128_pol && H3_AC && h3_args && var == V64 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
                     (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
   const int tbn = k128 ? 128 : bn;
   for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < tbn ? a0.W : tbn;
   pr.nb0 = a0.B * (P / tbn);
-  static const int max_ksplit = [] {
-    const char* ks = getenv("INFLOW_FUSED_KSPLIT");     // debug knob: cap phase C's K split
-    const int v = ks ? atoi(ks) : 8;
-    return v < 1 ? 1 : v;
-  }();
-  pr.max_ksplit = max_ksplit;
-  static const int dbg = [] {
-    const char* e = getenv("INFLOW_FUSED_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  pr.dbg = dbg;
+  pr.max_ksplit = 8;
+  pr.dbg = a0.exact_scale ? 16 : 0;        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile
   pr.reverse = a0.tile_order;
-  static const bool timing = getenv("INFLOW_FUSED_TIMING") != nullptr;
   pr.tbuf = nullptr;
-  if (timing) pr.tbuf = timing_buf(pr.nb0 * nnets);
+  if (INFLOW_PHASE_STAMPS) pr.tbuf = timing_buf(pr.nb0 * nnets);   // tools/build_alt_k128.py "stamps" builds only
   const unsigned nb = (unsigned)(pr.nb0 * nnets);
-  static const int split_h = [] {
-    const char* e = getenv("INFLOW_SPLIT_H");             // tuning knob: split-bf16 in the 32-px 2-WG/CU variant
-    return e ? atoi(e) : 1;
-  }();
-  const bool split = pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr && (var != VHALF || split_h);
+  const bool split = pr.a[0].A1s != nullptr && pr.a[1].A1s != nullptr;
   const bool h3 = split && pr.a[0].A1h != nullptr && pr.a[1].A1h != nullptr;
-  static const int quad_env = [] {
-    const char* e = getenv("INFLOW_FUSED_NW");            // tuning knob: 4 = one wave per SIMD (64-px tiles)
-    return e ? atoi(e) : 8;
-  }();
-  const bool quad = quad_env == 4;
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
   if (k128) {
@@ -1196,8 +1158,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   }
 #define L313S(TM_, MODE_, SPL_)                                                                         \
   do {                                                                                                  \
-    if (var == V64 && quad && SPL_ < 2) hipLaunchKernelGGL((net313_kernel_q<TM_, MODE_, (SPL_ < 2 ? SPL_ : 1)>), dim3(nb), dim3(256), 0, s, pr); \
-    else if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
+    if (var == V64) hipLaunchKernelGGL((net313_kernel<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
     else if (var == VHALF) hipLaunchKernelGGL((net313_kernel_h<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr); \
     else hipLaunchKernelGGL((net313_kernel_w<TM_, MODE_, SPL_>), dim3(nb), dim3(512), 0, s, pr);           \
   } while (0)

@@ -402,47 +402,27 @@ __global__ void slab_reduce_kernel(const float* slab, int nsplit, long n, float*
   out[i] = (float)s;
 }
 
-static bool wgrad_valu3_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("INFLOW_WGRAD_VALU3");               // debug knob: 0 = one-tap kernel
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static bool wgrad_valu3r_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("INFLOW_WGRAD_VALU3R");              // debug knob: 0 = chunked 3-tap kernel
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   if (a.M <= WGV_MAXM && a.P > 1 && a.W % 8 == 0 && a.P == a.H * a.W && a.g_sample % 4 == 0 &&
       (reinterpret_cast<uintptr_t>(a.G) & 15) == 0) {   // float4 loads of G rows
-    const bool three = a.ks == 3 && a.x_sample % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0 &&
-                       wgrad_valu3_enabled();
+    const bool three = a.ks == 3 && a.x_sample % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
     const int nb = three ? (a.N / 3 + 255) / 256 : (a.N + 255) / 256;
     const long rows = (long)a.B * a.H;
     // the row-resident kernel pipelines rows within a wave, so it wants one resident round of waves
     // (256 CUs x 4 SIMDs x 3 waves at its 145 VGPRs = 768 workgroups) with more rows each
-    const bool resident = three && wgrad_valu3r_enabled() && (a.W == 32 || a.W == 16 || a.W == 8);
-    static const int wg_target = [] {
-      const char* e = getenv("INFLOW_WGRAD_VALU3R_WGS");          // tuning knob
-      return e ? std::max(1, atoi(e)) : 768;
-    }();
+    const bool resident = three && (a.W == 32 || a.W == 16 || a.W == 8);
+    constexpr int wg_target = 768;
     int nsplit = (int)std::max<long>(1, std::min<long>(rows, (resident ? wg_target : 2048) / std::max(1, nb)));
     if (nsplit > a.max_split) nsplit = a.max_split;
     a.nsplit = nsplit;
     const bool prof = prof_enabled();
     if (prof) prof_begin_launch(s);
-    if (three && wgrad_valu3r_enabled() && a.W == 32)
+    if (three && a.W == 32)
       hipLaunchKernelGGL(wgrad_valu3r_kernel<32>, dim3(nb, nsplit), dim3(256), 0, s, a);
-    else if (three && wgrad_valu3r_enabled() && a.W == 16)
+    else if (three && a.W == 16)
       hipLaunchKernelGGL(wgrad_valu3r_kernel<16>, dim3(nb, nsplit), dim3(256), 0, s, a);
-    else if (three && wgrad_valu3r_enabled() && a.W == 8)
+    else if (three && a.W == 8)
       hipLaunchKernelGGL(wgrad_valu3r_kernel<8>, dim3(nb, nsplit), dim3(256), 0, s, a);
     else if (three)
       hipLaunchKernelGGL(wgrad_valu3_kernel, dim3(nb, nsplit), dim3(256), 0, s, a);
@@ -465,10 +445,7 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
     const int bm = 64 * tmw, bn = 64 * tnw;
     const int mt = (a.M + bm - 1) / bm, nt = (a.N + bn - 1) / bn;
     const long nchunks = (long)a.B * a.P / WG_K;
-    static const int tiled_wgs = [] {
-      const char* e = getenv("INFLOW_WGRAD_TILED_WGS");           // tuning knob
-      return e ? std::max(1, atoi(e)) : 1024;
-    }();
+    constexpr int tiled_wgs = 1024;     // 768 / 1536 / 2048 measured the same
     int nsplit = (int)std::max<long>(1, std::min<long>(nchunks / 4, tiled_wgs / std::max(1, mt * nt)));
     if (nsplit > a.max_split) nsplit = a.max_split;
     a.nsplit = nsplit;

@@ -186,14 +186,14 @@ struct Net313Args {
   int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
                           //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
   int tile_order;         // 1: the 128-pixel kernel walks the tiles backwards (series terms alternate; args[0])
+  int exact_scale;        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile (args[0]; tests)
 };
 struct Net313Pair {
   Net313Args a[2];
   int nb0;                // workgroups of net 0; blocks >= nb0 run net 1
-  int max_ksplit;         // cap on phase C's K split (debug knob, INFLOW_FUSED_KSPLIT)
-  unsigned long long* tbuf;   // INFLOW_FUSED_TIMING: per-workgroup s_memtime stamps at phase boundaries
-  int dbg;                // timing-attribution knob (INFLOW_FUSED_DBG, wrong results when set): 1 skip the
-                          // d1 load, 2 skip the d2 load, 4 skip phase C, 8 skip the input staging
+  int max_ksplit;         // cap on phase C's K split (8)
+  unsigned long long* tbuf;   // INFLOW_PHASE_STAMPS builds only: per-workgroup s_memtime stamps at phase boundaries
+  int dbg;                // bit 16: the 128-pixel kernel's chunk-1 exact-scale path on every tile (results unchanged)
   int reverse;            // 128-pixel kernel: workgroup i runs tile nb - 1 - i (alternating series terms)
 };
 int net313_supported(int hid, int C, int H, int W);

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
-INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE = 1, 2, 3     # InfNetOption
+INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE, INF_OPT_K128_EXACT_SCALE = 1, 2, 3, 4   # InfNetOption
 INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
 CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 

@@ -113,7 +113,8 @@ int inf_net_set_mfma(InfNet* net, int mode);
 int inf_net_get_mfma(const InfNet* net);
 /* Per-net options (no process-wide switches: two threads driving different nets never share one).  Returns the
  * previous value, or -INF_ERR_INVALID for an unknown option or a value out of range.
- *   INF_OPT_FUSED_K128    which kernel runs the fused VJP and forward (EVAL) of 512-wide nets in INF_MFMA_F16X3:
+ *   INF_OPT_FUSED_K128    which kernel runs the fused VJP, forward (EVAL) and derivative-saving forwards (SAVE,
+ *                         EVALSAVE) of 512-wide nets in INF_MFMA_F16X3:
  *                         0 the 64-pixel kernel only; 1 the 128-pixel K-chunked kernel where its grid still covers
  *                         all 256 CUs (default, or INFLOW_FUSED_K128 at inf_net_create); 2 wherever its tile fits.
  *                         A paired launch (both branches of an imBlock) follows the first net's value.
@@ -128,11 +129,16 @@ int inf_net_get_mfma(const InfNet* net);
  *                         lowest iterate, stall and protective breaks and Banach fallback -- the reference's result
  *                         for a batch of one, so a sharded batch gives the single-process result row for row.
  *                         INFLOW_CONVERGENCE=per_sample at create selects it.
- * FUSED_K128 and EVAL_OVERLAP are performance knobs without a reference counterpart (the reference
+ *   INF_OPT_K128_EXACT_SCALE  0 (default) / 1: the 128-pixel kernel puts chunk 1's phase-A values at chunk 0's column
+ *                         scales and falls back to exact per-chunk scales only for a tile where a value would not fit
+ *                         fp16; 1 takes the exact-scale path on every tile (tests: both paths give the same results).
+ * Unknown values of INFLOW_FUSED_K128 (0/1/2), INFLOW_EVAL_OVERLAP (0/1) and INFLOW_CONVERGENCE (global/per_sample)
+ * make inf_net_create fail with INF_ERR_INVALID.
+ * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
  * runs the VJP as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322); results
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
-  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3
+  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);

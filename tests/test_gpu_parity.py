@@ -540,10 +540,10 @@ def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):
         _close(a, b, rel=1e-5)
 
 
-@pytest.mark.parametrize('skew', [False, True])
+@pytest.mark.parametrize('skew,exact_scale', [(False, 0), (True, 0), (False, 1)])
 @pytest.mark.parametrize('B', [2, 16])
 @pytest.mark.parametrize('block', [0, 1, 3])
-def test_fused_k128_vjp_matches_64px_kernel(block, B, skew):
+def test_fused_k128_vjp_matches_64px_kernel(block, B, skew, exact_scale):
     """The 128-pixel K-chunked kernel (fused313k.hip, INF_MFMA_F16X3: activations split into fp16 h / l planes in two
     256-row LDS chunks) against the 64-pixel kernel in the same arithmetic mode: the net forward, the VJP, the chained log-det
     series (each term stages the previous term's taps, preact swish' and trace partial) and the Neumann vector
@@ -552,7 +552,8 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew):
     max(1, |ref|_inf), the fp32-level bound of the other fused-vs-fused comparisons.
     skew: hidden units 256-511 of both hidden layers weighted 1000x (first conv's output rows, last conv's input
     channels), so the second 256-row chunk's column maxima far exceed the first's and the 128-pixel kernel's chunk 1
-    leaves its fast put at chunk 0's scales for the exact-scale path."""
+    leaves its fast put at chunk 0's scales for the exact-scale path.
+    exact_scale: INF_OPT_K128_EXACT_SCALE = 1 sends every tile through that path."""
     arch = syn.CIFAR10
     m, _ = _model(arch, B)
     blk = imblocks(m)[block]
@@ -581,6 +582,7 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew):
         _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
     outs = {}
     k_prev = net.get_option(_hip.INF_OPT_FUSED_K128)
+    assert net.set_option(_hip.INF_OPT_K128_EXACT_SCALE, exact_scale) == 0
     try:
         for pol in (2, 0):
             prev = net.set_option(_hip.INF_OPT_FUSED_K128, pol)
@@ -602,6 +604,7 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew):
             outs[pol] = (y, g, ld, w)
     finally:
         net.set_option(_hip.INF_OPT_FUSED_K128, k_prev)
+        net.set_option(_hip.INF_OPT_K128_EXACT_SCALE, 0)
     assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_K128, 3) < 0
     assert net.get_option(_hip.INF_OPT_FUSED_K128) == k_prev
     for a in outs[2]:

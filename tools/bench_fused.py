@@ -1,6 +1,6 @@
 """Per-scale timing of the paired log-det series (one fused VJP launch per term for both nets).
 
-    INFLOW_FUSED_BN=32 python tools/bench_fused.py      # tile-size A/B (the knob is read once per process)
+    python tools/bench_fused.py      # the tile variant is the engine's policy (fused313.hip launch_net313_multi)
 """
 import ctypes
 import os
@@ -54,4 +54,4 @@ for B in (64, 256):
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1) / 3
         row.append('s%d %.3f ms/series (%.1f us/term)' % (bi // 2, ms, ms / NT * 1e3))
-    print('B=%d bn=%s  ' % (B, os.environ.get('INFLOW_FUSED_BN', 'auto')) + '  '.join(row), flush=True)
+    print('B=%d  ' % B + '  '.join(row), flush=True)

@@ -9,7 +9,10 @@ shipped: the product source stays untouched; a patched copy is compiled into gpu
       dsyncN first-round workgroups of every other CU group start N k-cycles late (desynchronised bursts)
       DNAME=V  #define NAME V ahead of the source (the product's compile-time switches)
       sub    INFLOW_K128_SUBSTAMPS: stamps inside chunk 1 and phase C (results unchanged; sched_barrier fences)
-Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py, INFLOW_FUSED_TIMING=1 for the phase stamps).
+      stamps no patch (the phase stamps only)
+Every alternative library is built with INFLOW_PHASE_STAMPS=1 (fused313.hip / fused313k.hip s_memtime stamps at
+the phase boundaries, printed per kernel at exit); `python tools/build_alt_k128.py stamps stamps` gives the product
+kernels with stamps.  Run with INFLOW_LIB=gpurun_alt/lib_<name>.so (tools/series_only.py).
 """
 import os
 import subprocess
@@ -61,12 +64,16 @@ def main():
         f.write(src)
     os.makedirs(os.path.join(R, 'gpurun_alt'), exist_ok=True)
     obj = '/tmp/alt_%s.o' % name
+    obj2 = '/tmp/alt_%s_fused313.o' % name
+    flags = ['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=fast',
+             '-DINFLOW_PHASE_STAMPS=1', '-c']
     try:
-        subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC',
-                        '-ffp-contract=fast', '-c', '-o', obj, tmp], check=True)
+        subprocess.run(flags + ['-o', obj, tmp], check=True)
     finally:
         os.remove(tmp)
-    objs = [os.path.join(O, f) for f in sorted(os.listdir(O)) if f.endswith('.o') and f != 'fused313k.o']
+    subprocess.run(flags + ['-o', obj2, os.path.join(C, 'fused313.hip')], check=True)
+    objs = [obj2] + [os.path.join(O, f) for f in sorted(os.listdir(O))
+                     if f.endswith('.o') and f not in ('fused313k.o', 'fused313.o')]
     out = os.path.join(R, 'gpurun_alt', 'lib_%s.so' % name)
     subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-shared', '-fPIC', '-o', out, obj] + objs, check=True)
     print('built', out)

@@ -6,6 +6,6 @@ for L in cur "$@"; do
   E=""; [ $L != cur ] && E="INFLOW_LIB=$GRAFT_REPO_ROOT/gpurun_alt/lib_$L.so"
   for S in 0 1 2; do
     env $E timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 5 2>&1 | grep -a "us/term" | sed "s/^/$L /" || exit 1
-    env $E INFLOW_FUSED_TIMING=1 timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "mode2 split" | sed "s/^/$L /" || exit 1
+    env $E timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "mode2 split" | sed "s/^/$L /" || exit 1
   done
 done

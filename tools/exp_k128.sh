@@ -8,5 +8,5 @@ for S in 0 1; do
     timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 5 2>&1 | grep -a "us/term" | sed 's/^/k128 /' || exit 1
     INFLOW_FUSED_K128=0 timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 5 2>&1 | grep -a "us/term" | sed "s/^/k64  /" || exit 1
   done
-  INFLOW_FUSED_TIMING=1 timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "mode2" || exit 1
+  INFLOW_LIB=gpurun_alt/lib_stamps.so timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "mode2" || exit 1
 done

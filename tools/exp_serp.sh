@@ -1,5 +1,5 @@
 # per-term series time (s0/s1 pair) and phase stamps of the tree's library; k128 parity subset
 cd $GRAFT_REPO_ROOT
 for S in 0 1; do timeout -k 5 90 python3 tools/series_only.py --scale $S --mfma 2 --reps 10 2>&1 | grep -a "us/term" || exit 1; done
-for S in 0 1; do INFLOW_FUSED_TIMING=1 timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "var3 mode2" | cut -c1-200 || exit 1; done
+for S in 0 1; do INFLOW_LIB=gpurun_alt/lib_stamps.so timeout -k 5 60 python3 tools/series_only.py --scale $S --mfma 2 --reps 1 2>&1 | grep -a "var3 mode2" | cut -c1-200 || exit 1; done
 timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k128 or headline or golden" 2>&1 | tail -3
