@@ -107,10 +107,13 @@ def parse():
     ap.add_argument('--config', default='cifar10', choices=sorted(BENCH_CONFIGS))
     ap.add_argument('--probes', default='device', choices=['device', 'reference'])
     ap.add_argument('--cpu-baseline', type=int, default=1, help='time the oracle on the host (rank 0, N=1)')
-    ap.add_argument('--cpu-batch', type=int, default=8,
-                    help='images per timed CPU-baseline batch (1 warm-up batch of half that, then the median of 3); '
-                         'per-sample CPU time is batch-independent from 8 to 64 images '
-                         '(profiles/r04/cpu_baseline_batch.json); tabular configs time the bench batch itself')
+    ap.add_argument('--cpu-batch', type=int, default=64,
+                    help='images per timed CPU-baseline batch (BASELINE.md:36-38: B = 64; one warm-up batch of 8, then '
+                         'the median of --cpu-reps batches).  Per-sample CPU time is NOT batch-independent on the GPU '
+                         'box (B = 8: 4.3 samples/s, B = 64: 1.4 samples/s on 16 threads, '
+                         'profiles/r04/cpu_baseline_batch.json), so the protocol batch is kept.  Tabular configs time '
+                         'the bench batch itself')
+    ap.add_argument('--cpu-reps', type=int, default=3, help='timed CPU-baseline batches (median)')
     ap.add_argument('--train-step', default='full', choices=['full', 'fwdbwd'],
                     help='train mode: full = forward + backward + clip_grad_norm_(1) + Adam + update_lipschitz + '
                          'EMA (train_img.py:637-658); fwdbwd = forward + backward only')
@@ -131,12 +134,11 @@ def host_threads():
     return max(1, n)
 
 
-def cpu_baseline(arch, sd, model, device, nimg):
+def cpu_baseline(arch, sd, model, device, nimg, reps=3):
     """Oracle (CPU restatement, torch fp32, autograd VJPs) timed as BASELINE.md's CPU-baseline plan prescribes --
-    N = nproc threads, one warm-up batch, then the median of 3 batches.  Images: batches of `nimg` (per-sample
-    CPU time does not depend on the batch from 8 to 64 images, profiles/r04/cpu_baseline_batch.json; a B = 64
-    batch takes minutes of CPU).  Tabular: the bench batch itself.  Also runs the GPU path on the last batch with
-    the reference RNG replay -> |loss_gpu - loss_oracle| (bits/dim or nats)."""
+    N = nproc threads, one warm-up batch, then the median of `reps` batches of `nimg` (images: B = 64, ~45 s each
+    on 16 threads; the warm-up batch is 8 images).  Tabular: the bench batch itself.  Also runs the GPU path on the
+    last batch with the reference RNG replay -> |loss_gpu - loss_oracle| (bits/dim or nats)."""
     from oracle import inflow_oracle as orc
     cores = host_threads()
     torch.set_num_threads(cores)
@@ -145,7 +147,7 @@ def cpu_baseline(arch, sd, model, device, nimg):
         flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
         batch = lambda n, seed: syn.image_batch(n, arch['input_size'], arch['nvals'], seed=seed)
         run = lambda xb: orc.image_bits_per_dim(flow, xb, arch['nvals'])
-        warm_n = max(1, nimg // 2)
+        warm_n = min(8, nimg)
     else:
         flow = orc.build(arch, sd, syn.fc_flow_layout(arch))
         batch = lambda n, seed: syn.tabular_batch(n, arch['d'], seed=seed)
@@ -155,7 +157,7 @@ def cpu_baseline(arch, sd, model, device, nimg):
     torch.manual_seed(10)
     run(batch(warm_n, 776))                                    # warm-up batch (untimed)
     times = []
-    for r in range(3):
+    for r in range(reps):
         x = batch(nimg, 777 + r)
         np.random.seed(11 + r)
         torch.manual_seed(11 + r)
@@ -164,8 +166,8 @@ def cpu_baseline(arch, sd, model, device, nimg):
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times))
     set_probe_mode('reference')
-    np.random.seed(11 + 2)
-    torch.manual_seed(11 + 2)
+    np.random.seed(11 + reps - 1)
+    torch.manual_seed(11 + reps - 1)
     if image:
         gpu_loss, _, _ = image_logpx(model, x.to(device), arch['nvals'])
     else:
@@ -177,8 +179,9 @@ def cpu_baseline(arch, sd, model, device, nimg):
     return ({'value': nimg / dt, 'unit': 'samples/s', 'cores': cores, 'nproc': cores, 'threads': cores,
              'os_cpu_count': os.cpu_count(), 'kind': 'port',
              'sample': 'oracle/inflow_oracle.py (torch fp32 CPU, torch.set_num_threads(nproc = %d)) on %s: one '
-                       'warm-up batch of %d, then the median of 3 batches of %d %s (%.1f / %.1f / %.1f s)'
-                       % (cores, what, warm_n, nimg, 'images' if image else 'rows', *times)},
+                       'warm-up batch of %d, then the median of %d batches of %d %s (%s s)'
+                       % (cores, what, warm_n, reps, nimg, 'images' if image else 'rows',
+                          ' / '.join('%.1f' % t for t in times))},
             abs(float(gpu_loss) - float(ref_loss)), float(ref_loss))
 
 
@@ -272,17 +275,33 @@ def main():
             _, logpx, _ = image_logpx(model, xs[i % xs.shape[0]], arch['nvals'])
         else:
             _, logpx, _ = tabular_logpx(model, xs[i % xs.shape[0]])
-        s, n = dd.global_logpx_sum(logpx)      # the one collective per batch
+        return dd.global_logpx_pair(logpx)     # the one collective per batch (its readback enqueued behind it)
+
+    def loss_of(pair):
+        s, n = pair.get()
         return dd.bits_per_dim(s, n, ndim) if image else -s / n
 
-    for i in range(args.warmup):
-        step(i)
+    def run_steps(first, count):
+        """Eval: batch j's all-reduced [sum log p, N] is read on the host after batch j + 1 is enqueued, so the GPU
+        does not drain between batches while the host prepares the next one; every batch's value is read."""
+        pending, last = None, None
+        for i in range(first, first + count):
+            out = step(i)
+            if args.mode == 'train':
+                last = out
+                continue
+            if pending is not None:
+                last = loss_of(pending)
+            pending = out
+        if pending is not None:
+            last = loss_of(pending)
+        return last
+
+    run_steps(0, args.warmup)
     dd.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    bpd = None
-    for i in range(args.steps):
-        bpd = step(args.warmup + i)
+    bpd = run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     dd.barrier()
     elapsed = dd.max_over_ranks(time.perf_counter() - t0, device)
@@ -298,7 +317,7 @@ def main():
     overlap_on = any(v == 1 for v in overlap_prev.values())
     _hip.profile_begin(100000)
     t1 = time.perf_counter()
-    step(0)
+    run_steps(0, 1)
     torch.cuda.synchronize()
     prof_wall = time.perf_counter() - t1
     stats = _hip.profile_end()
@@ -374,6 +393,9 @@ def main():
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),
                  'gemm_flop_rate_tflops': round(total_gemm_flops / (prof_wall * 1e12), 2),
                  'kernel_busy_frac': round(total_kernel_ms / (prof_wall * 1e3), 3),
+                 'kernel_busy_basis': ('sum of kernel times / wall time of the extra sequential-schedule profiling '
+                                       'step; the timed (overlapped) steps: rocprofv3 kernel trace, '
+                                       'profiles/r04/timeline_timed_window.json'),
                  'kernels': sorted([{'kernel': _hip.tag_name(s['tag']), 'launches': s['launches'],
                                      'ms': round(s['total_ms'], 3),
                                      'tflops': round(s['flops'] / (s['total_ms'] * 1e9), 2) if s['flops'] else None,
@@ -382,7 +404,7 @@ def main():
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline and arch_name != 'celebahq256' and args.mode == 'eval':
-        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch if image else B)
+        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch if image else B, args.cpu_reps)
         out['cpu_baseline'] = cb
         out['bpd_delta_vs_oracle' if image else 'nats_delta_vs_oracle'] = delta
         out['speedup_vs_cpu_baseline'] = round(value / cb['value'], 1)

@@ -114,6 +114,8 @@ struct InfNet {
   int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
+  // fused fc path (fcnet.hip): the whole net in one launch per evaluation (forward and forward-mode Jacobian)
+  bool fcfused = false;
 };
 
 namespace {
@@ -275,8 +277,32 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   return f;
 }
 
+FcArgs fc_args(const InfNet* n, const float* x, int B) {
+  FcArgs f;
+  memset(&f, 0, sizeof(f));
+  f.nl = (int)n->L.size();
+  f.d = n->d;
+  f.B = B;
+  f.act = n->L[0].act;
+  for (int l = 0; l < f.nl && l < FC_MAXL; ++l) {
+    f.L[l].A = n->L[l].f.A;
+    f.L[l].Kpad = n->L[l].f.Kpad;
+    f.L[l].b = n->L[l].b;
+    f.L[l].beta = n->L[l].act_beta;
+  }
+  f.x = x;
+  return f;
+}
+
 int run_forward(InfNet* n, const float* x, int B, Bufs& bf, int mode, const OutArgs* oa, hipStream_t s) {
   const int L = (int)n->L.size();
+  if (n->fcfused && mode >= OM_PLAIN && mode <= OM_RECOMP) {   // the whole net and fc_out's epilogue in one launch
+    FcArgs f = fc_args(n, x, B);
+    f.o = *oa;
+    f.o.mode = mode;
+    f.o.bias = n->L[L - 1].b;
+    return launch_fcnet(f, false, s);
+  }
   if (n->fused) {
     Net313Args f = net313_args(n, x, B, bf, false);
     INF_TRY(launch_net313(f, n->fhid, mode < 0 ? MODE_SAVE : MODE_EVAL, s));
@@ -1193,6 +1219,24 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     if (first) n->rows_max = std::max(n->rows_max, w.g.M);
   }
   if (L == 1) n->hidden_max = std::max(n->hidden_max, 1);
+  // fused fc net (fcnet.hip): 128-wide hidden layers with one activation kind, no input pre-activation
+  {
+    const char* off = getenv("INFLOW_NO_FUSED");
+    bool ok = n->fc && n->pre_act == ACT_NONE && L >= 2 && L <= FC_MAXL && !(off && off[0] == '1');
+    for (int l = 0; ok && l < L; ++l) {
+      const WLayer& w = n->L[l];
+      if (l < L - 1 && (w.cout != 128 || w.act != n->L[0].act)) ok = false;
+    }
+    if (ok) {
+      FcArgs f;
+      memset(&f, 0, sizeof(f));
+      f.nl = L;
+      f.d = n->d;
+      f.act = n->L[0].act;
+      for (int l = 0; l < L; ++l) f.L[l].Kpad = n->L[l].f.Kpad;
+      n->fcfused = fcnet_supported(f, false) != 0;
+    }
+  }
   // fused 3-1-3 conv net (run_cifar10.sh nets): 3x3 C->H, swish, 1x1 H->H, swish, 3x3 H->C
   {
     const char* off = getenv("INFLOW_NO_FUSED");
@@ -1701,6 +1745,52 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
   return series_fused(nets, xs, es, 2, coeff, n_terms, outs, B, bfs, s, /*save_mask=*/2u);
 }
 
+int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B,
+                           int T, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
+  if (!nx || !nz || !x || !z || !logdet_x || !logdet_z || B <= 0 || T <= 0 || T > 64 || !same_shape(nx, nz))
+    return INF_ERR_INVALID;
+  if (!nx->fcfused || !nz->fcfused || nx->d > 10) return INF_ERR_UNSUPPORTED;
+  {
+    FcArgs probe = fc_args(nx, x, B);
+    FcArgs probe_z = fc_args(nz, x, B);
+    if (!fcnet_supported(probe, true) || !fcnet_supported(probe_z, true)) return INF_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  int st = INF_OK;
+  const float* xi = to_internal(nz, x, bf.xin, B, s, &st);
+  INF_TRY(st);
+  // log|det(I + J_fx(x))| first: it depends only on x (implicit_block.py:358-362)
+  FcArgs fjx = fc_args(nx, xi, B);
+  fjx.logdet = logdet_x;
+  INF_TRY(launch_fcnet(fjx, true, s));
+  // x_embed = f_x(x) + x, the root solve, z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:71, 74-80, 227)
+  OutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in0 = xi;
+  a.out0 = bf.fx;
+  a.out1 = bf.xemb;
+  INF_TRY(run_forward(nx, xi, B, bf, OM_EMBED, &a, s));
+  InfBroydenStats sst = stats_for(stats);
+  INF_TRY(broyden_solve(nz, xi, B, T, eps, &sst, nullptr, bf, s));
+  if (stats) *stats = sst;
+  if (!sst.prot_break) {
+    INF_TRY(glue_recomp(bf.fx, bf.flow, xi, bf.tmp, (long)B * nx->d, s));
+  } else {
+    memset(&a, 0, sizeof(a));
+    a.in0 = bf.fx;
+    a.in1 = xi;
+    a.out0 = bf.tmp;
+    INF_TRY(run_forward(nz, bf.lowest, B, bf, OM_RECOMP, &a, s));
+  }
+  // log|det(I + J_fz(z))| at the recomputed z
+  FcArgs fjz = fc_args(nz, bf.tmp, B);
+  fjz.logdet = logdet_z;
+  INF_TRY(launch_fcnet(fjz, true, s));
+  return to_boundary(nx, bf.tmp, z, B, s);
+}
+
 int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
                       int B, void* ws, size_t ws_bytes, void* stream) {
   if (!n || !x || !vareps || !coeff || !out || B <= 0 || n_terms < 0 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
@@ -1842,6 +1932,15 @@ static int fc_jacobian(InfNet* n, const float* x, int B, Bufs& bf, const float**
   int st = INF_OK;
   const float* xi = to_internal(n, x, bf.xin, B, s, &st);
   INF_TRY(st);
+  if (n->fcfused) {
+    FcArgs f = fc_args(n, xi, B);
+    f.tang = bf.ext1;
+    if (fcnet_supported(f, true)) {
+      INF_TRY(launch_fcnet(f, true, s));
+      *tang = bf.ext1;
+      return INF_OK;
+    }
+  }
   INF_TRY(glue_init_tangents(xi, bf.ext0, d, B, s));
   const int cols = (d + 1) * B;
   const float* cur = bf.ext0;
@@ -1878,6 +1977,14 @@ int inf_logdet_exact(InfNet* n, const float* x, float* out, int B, void* ws, siz
   hipStream_t s = (hipStream_t)stream;
   Bufs bf;
   if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  if (n->fcfused) {                   // forward-mode Jacobian and the LU in one launch
+    int st = INF_OK;
+    const float* xi = to_internal(n, x, bf.xin, B, s, &st);
+    INF_TRY(st);
+    FcArgs f = fc_args(n, xi, B);
+    f.logdet = out;
+    if (fcnet_supported(f, true)) return launch_fcnet(f, true, s);
+  }
   const float* tang = nullptr;
   INF_TRY(fc_jacobian(n, x, B, bf, &tang, s));
   return launch_logdet_small(tang, out, n->d, B, B, s);

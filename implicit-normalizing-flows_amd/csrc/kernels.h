@@ -206,6 +206,27 @@ int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets = 0);
 
 // ------------------------------------------------------------------------------------------
+// fused fc net (fcnet.hip): the tabular / toy nets, one launch per evaluation
+// ------------------------------------------------------------------------------------------
+constexpr int FC_MAXL = 8;
+struct FcLayer {
+  const float* A;         // the layer's forward operand, row-major (Mpad, Kpad) (Lipschitz-normalised W)
+  int Kpad;
+  const float* b;         // bias
+  const float* beta;      // swish beta (hidden layers of Swish nets)
+};
+struct FcArgs {
+  int nl, d, B, act;      // layers, features, batch, Act of the hidden layers
+  FcLayer L[FC_MAXL];
+  const float* x;         // (d, B) feature-major input
+  OutArgs o;              // FWD: fc_out's epilogue (o.Y unused: the net output stays in LDS)
+  float* logdet;          // JAC (optional): log|det(I + J_f(x))| per sample
+  float* tang;            // JAC (optional): (d, (d + 1) B) = [f(x) | df/dx_1 | ...], fc_jacobian's layout
+};
+int fcnet_supported(const FcArgs& a, bool jac);
+int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
 // parameter gradients (grad.hip)
 // ------------------------------------------------------------------------------------------
 struct WgradArgs {

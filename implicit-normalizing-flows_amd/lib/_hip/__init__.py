@@ -100,6 +100,8 @@ _SIGS = {
     'inf_imblock_eval': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, _P,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(BroydenStats), _P,
                                         ctypes.c_size_t, _P]),
+    'inf_imblock_eval_exact': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                              ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_imblock_backward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                             ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_imblock_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
@@ -361,6 +363,8 @@ def tag_name(tag):
         #                      53x: net313k (128-px K-chunked VJP, fused313k.hip)
         return 'net313%s<%s>' % (['_kernel', '_kernel_h', '_kernel_w', 'k_kernel'][(tag - 500) // 10],
                                  ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
+    if tag in (600, 601):    # fused fc net (fcnet.hip): forward + fc_out epilogue / forward-mode Jacobian + LU
+        return 'fcnet_kernel<%s>' % ('FWD', 'JAC')[tag - 600]
     if tag == 899:
         return 'wgrad_valu_kernel'
     if 800 <= tag < 900:     # weight-gradient kernel (grad.hip), 8<TMW><TNW>

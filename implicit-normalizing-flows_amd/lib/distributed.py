@@ -43,39 +43,55 @@ def shard(n_total, rank, world_size):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def global_logpx_sum(logpx_local):
-    """All-reduce [sum log p(x), N] (fp64) over the default group; returns python floats.
+class PendingPair:
+    """[sum log p(x), N] of one batch: all-reduced on the device, its 16-byte copy to pinned host memory enqueued
+    behind it; get() waits for that copy only.  An evaluation loop that calls get() for batch i after enqueueing batch
+    i + 1 never lets the GPU drain between batches (the host's Python for the next batch overlaps this batch's tail)."""
+
+    _ring = {}
+
+    def __init__(self, t):
+        dev = t.device
+        if dev.type != 'cuda':
+            self.host, self.ev = t, None
+            return
+        ring = PendingPair._ring.get(dev.index)
+        if ring is None:
+            ring = PendingPair._ring[dev.index] = [[torch.empty(2, dtype=torch.float64, pin_memory=True), 0]
+                                                   for _ in range(4)]
+        slot = min(ring, key=lambda r: r[1])          # the least recently used of 4 pinned buffers
+        slot[1] = max(r[1] for r in ring) + 1
+        self.host = slot[0]
+        self.host.copy_(t, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(dev))
+
+    def get(self):
+        if self.ev is not None:
+            if os.environ.get('INFLOW_BLOCKING_WAIT', '') == '1':
+                self.ev.synchronize()
+            else:                  # poll: a long blocking wait wakes up late (see engine.hip host_wait)
+                while not self.ev.query():
+                    pass
+        return float(self.host[0]), float(self.host[1])
+
+
+def global_logpx_pair(logpx_local):
+    """All-reduce [sum log p(x), N] (fp64) over the default group and enqueue its readback; returns a PendingPair.
 
     The pair is built on the device (a fill, not a pageable host-to-device copy, which would wait for the
-    whole queue) and read back with one 16-byte copy."""
+    whole queue)."""
     t = torch.empty(2, dtype=torch.float64, device=logpx_local.device)
     t[0] = logpx_local.sum(dtype=torch.float64)
     t[1].fill_(float(logpx_local.numel()))
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return _readback(t)
+    return PendingPair(t)
 
 
-_PINNED = {}
-
-
-def _readback(t):
-    """Two fp64 device values -> python floats through a pinned host buffer (an asynchronous copy plus an event
-    wait, polled rather than blocking: after a long wait the blocking form returns late, with the GPU idle)."""
-    if t.device.type != 'cuda':
-        return tuple(t.tolist())
-    buf = _PINNED.get(t.device.index)
-    if buf is None:
-        buf = _PINNED[t.device.index] = torch.empty(2, dtype=torch.float64, pin_memory=True)
-    buf.copy_(t, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(t.device))
-    if os.environ.get('INFLOW_BLOCKING_WAIT', '') == '1':
-        ev.synchronize()
-    else:                      # poll: a long blocking wait wakes up late (see engine.hip host_wait)
-        while not ev.query():
-            pass
-    return float(buf[0]), float(buf[1])
+def global_logpx_sum(logpx_local):
+    """All-reduce [sum log p(x), N] (fp64) over the default group; returns python floats."""
+    return global_logpx_pair(logpx_local).get()
 
 
 def bits_per_dim(sum_logpx, count, ndim):

@@ -486,6 +486,10 @@ class imBlock(nn.Module):
             out = self._eval_fused(nx, nz, x, stream)
             if out is not None:
                 return out[0], logpx - out[1]
+        if logpx is not None and not self.training and x.dim() == 2 and x.shape[1] <= 10:
+            out = self._eval_exact(nx, nz, x, stream)
+            if out is not None:
+                return out[0], logpx - out[1]
         with torch.no_grad():
             z = self._root(nz, nx, x, self.eps_forward, stream, forward=True)
         if self.training:       # keep the frozen copies in step (implicit_block.py:228-229)
@@ -493,6 +497,24 @@ class imBlock(nn.Module):
         if logpx is None:
             return z
         return z, logpx - self._logdetgrad(z, x)
+
+    def _eval_exact(self, nx, nz, x, stream):
+        """Eval forward + exact log-det of an fc block (d <= 10: implicit_block.py:249-260 in eval) in one engine call
+        (inf_imblock_eval_exact); no RNG is drawn on this branch.  None when the engine declines (separate calls)."""
+        x = x.contiguous()
+        B, T = x.shape[0], int(self.threshold)
+        ws = _hip.workspace(x.device, nz.ws_bytes(B, T))
+        z = torch.empty_like(x)
+        out = torch.empty(2, B, device=x.device)
+        st = _stats(B, (nz,))
+        rc = _hip.load().inf_imblock_eval_exact(nx.handle, nz.handle, _hip.ptr(x), _hip.ptr(z), _hip.ptr(out[0]),
+                                                _hip.ptr(out[1]), B, T, float(self.eps_forward), ctypes.byref(st),
+                                                _hip.ptr(ws), ws.numel(), stream)
+        if rc == _hip.INF_ERR_UNSUPPORTED:
+            return None
+        _hip.check(rc, 'inf_imblock_eval_exact')
+        self.last_broyden = st.as_dict(T)
+        return z, (out[0] - out[1]).view(-1, 1)
 
     def _eval_fused(self, nx, nz, x, stream):
         """Eval forward + log-det in one engine call (inf_imblock_eval) when both nets are fused.  The series

@@ -200,6 +200,16 @@ int inf_logdet_series_pair(InfNet* net_a, const float* x_a, const float* vareps_
 int inf_imblock_eval(InfNet* net_x, InfNet* net_z, const float* x, float* z, const float* eps_x, const float* eps_z,
                      const float* coeff, int n_terms, float* logdet_x, float* logdet_z, int batch, int threshold,
                      double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
+/* The whole eval pass of an imBlock on fc nets with d <= 10 (the tabular / toy configs; implicit_block.py:220-234
+ * with the exact branch of 245-260, 358-362): log|det(I + J_fx(x))| into logdet_x, the root solve,
+ * z = (f_x(x) - f_z(z*)) + x, and log|det(I + J_fz(z))| into logdet_z (the block's log-det is their difference).
+ * x, z are (batch, d).  Every net evaluation and both Jacobian log-dets are single launches of the fused fc
+ * kernel (fcnet.hip); the x-branch log-det is enqueued ahead of the root solve, so the GPU works on it while the
+ * host waits for the solver's residual norms.  INF_ERR_UNSUPPORTED when a net is not on the fused fc path (use the
+ * separate calls).  ws >= inf_workspace_bytes(net_z, batch, threshold). */
+int inf_imblock_eval_exact(InfNet* net_x, InfNet* net_z, const float* x, float* z, float* logdet_x, float* logdet_z,
+                           int batch, int threshold, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes,
+                           void* stream);
 /* Neumann gradient surrogate value (implicit_block.py:429-438): w = sum_{k=0}^{n} ncoeff[k] (J^T)^k eps,
  * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
 int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,

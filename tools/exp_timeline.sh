@@ -1,4 +1,5 @@
-# rocprofv3 kernel trace of the default bench, then the idle-gap analysis
+# rocprofv3 kernel trace of the default bench's timed steps (overlapped eval schedule), then the idle-gap analysis:
+# the union of kernel intervals over the trace after warm-up is the GPU busy fraction of the timed steps
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/tl
