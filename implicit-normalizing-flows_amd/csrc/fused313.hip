@@ -1125,10 +1125,8 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   // VJP / EVAL variant policy (per net, INF_OPT_FUSED_K128): 0 the 64-pixel kernel only, 1 the 128-pixel
   // K-chunked kernel where its grid still covers every CU (default), 2 wherever it fits (tests)
   const int k128_pol = a0.k128;
-  const bool forced = k128_pol == 2 || k128_pol == 4;
   const bool k128 = k128_pol && H3_AC && h3_args && var == V64 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
-                    (forced || (long)nnets * a0.B * (P / 128) >= 256);
-  const bool pipe = k128 && mode == MODE_VJP && k128_pol >= 3 && net313p_fits(hid, a0.C, a0.H, a0.W);
+                    (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
   const int tbn = k128 ? 128 : bn;
   for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < tbn ? a0.W : tbn;
   pr.nb0 = a0.B * (P / tbn);
@@ -1143,8 +1141,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
   if (k128) {
-    if (pipe) INF_TRY(launch_net313p(pr, nb, s));
-    else INF_TRY(launch_net313k(pr, mode, nb, s));
+    INF_TRY(launch_net313k(pr, mode, nb, s));
     if (pr.tbuf) {
       char key[64];
       snprintf(key, sizeof(key), "var3 mode%d split2 C%d", mode, a0.C);
@@ -1155,7 +1152,7 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
       const double fC = mode == MODE_SAVE ? 0.0 : 2.0 * 9.0 * a0.C * hid;
       const double f = 2.0 * hid * 9.0 * a0.C + 2.0 * hid * hid + fC;
       const double bytes = 4.0 * npx * (a0.C + (mode == MODE_EVAL ? 0.0 : 2.0 * hid) + (mode == MODE_SAVE ? 0.0 : 9.0 * a0.C));
-      prof_end_launch(s, (pipe ? 540 : 530) + mode, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+      prof_end_launch(s, 530 + mode, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
     }
     return INF_OK;
   }

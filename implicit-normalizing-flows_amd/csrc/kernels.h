@@ -184,8 +184,7 @@ struct Net313Args {
   float* acc_w;           // with in_taps: acc_w[img, own pixels] += acc_coef * v (Neumann vector accumulation,
   float acc_coef;         //   implicit_block.py:430-436), v the previous term's VJP after the tap sum
   int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
-                          //   covers every CU, 2 128-px wherever it fits, 3 / 4 as 1 / 2 with the VJP on the
-                          //   pipelined 128-px kernel (fused313p.hip); a pair launch follows args[0]
+                          //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
   int tile_order;         // 1: the 128-pixel kernel walks the tiles backwards (series terms alternate; args[0])
   int exact_scale;        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile (args[0]; tests)
 };
@@ -201,9 +200,6 @@ int net313_supported(int hid, int C, int H, int W);
 // 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
 int net313k_fits(int hid, int C, int H, int W);
 int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s);
-// pipelined 128-pixel VJP (fused313p.hip): four 128-row chunks, two chunk buffers, SIMD partners staggered
-int net313p_fits(int hid, int C, int H, int W);
-int launch_net313p(const Net313Pair& pr, unsigned nb, hipStream_t s);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 // layout_nets (> 0) picks the tile variant as if that many nets shared the grid: launches that write
 // derivatives for a paired series must use the pair's variant (the d1/d2 layout depends on it)
