@@ -110,20 +110,20 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
 #define STAMP(i_)                                                                            \
   do {                                                                                       \
-    if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
   // per-wave stamps (lane 0 of every wave): slot 8 + w at its phase-B end, 16 + w once its epilogue-B
   // multiplier has arrived
 #define WSTAMP(base_)                                                                         \
   do {                                                                                       \
-    if (INFLOW_PHASE_STAMPS && pr.tbuf && (threadIdx.x & 63) == 0) {                                                \
+    if (pr.tbuf && (threadIdx.x & 63) == 0) {                                                \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                            \
       pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + (threadIdx.x >> 6)] = t_;                \
       if (NW == 4) pr.tbuf[(long)blockIdx.x * TSLOTS + (base_) + 4 + (threadIdx.x >> 6)] = t_; \
     }                                                                                        \
   } while (0)
   STAMP(0);
-  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int P = a.H * a.W;
@@ -732,7 +732,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           if constexpr (MODE == MODE_VJP) acc[m][b][r] = acc[m][b][r] * dmul[m][b][r];
           else acc[m][b][r] = swish_fast_f(acc[m][b][r] + a.b2[o], sp2);
         }
-    if (INFLOW_PHASE_STAMPS && pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
+    if (pr.tbuf) {       // (timing build only: make the stamp wait for the multiplies)
       float s_ = 0.f;
 #pragma unroll
       for (int m = 0; m < TM; ++m)
@@ -986,7 +986,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     }   // rounds
   }
   STAMP(7);
-  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
 #undef STAMP
 #undef WSTAMP
 }

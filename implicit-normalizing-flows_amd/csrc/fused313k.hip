@@ -100,19 +100,21 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   __shared__ __attribute__((aligned(16))) float smem[KB_LDS];
 #define KSTAMP(i_)                                                                             \
   do {                                                                                         \
-    if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + (i_)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-  // stamps 8..15 inside chunk 1 and phase C (INFLOW_PHASE_STAMPS builds), fenced with sched_barrier: the fences stay in every
+  // stamps 8..15 inside chunk 1 and phase C (INFLOW_PHASE_STAMPS builds; pr.tbuf is null otherwise, but the guarded
+  // stores stay in the code: without them the register allocator spills 24 instead of 9 VGPRs), fenced with
+  // sched_barrier: the fences stay in every
   // build, they keep the compiler from hoisting the next phase's loads into the current one (measured faster with
   // them: 308 vs 321 us per s0 series term, 110 vs 114 at s1)
 #define KSUB(i_)                                                                               \
   do {                                                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                         \
-    if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + (i_)] = __builtin_amdgcn_s_memtime(); \
+    if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + (i_)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                         \
   } while (0)
   KSTAMP(0);
-  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
+  if (pr.tbuf && threadIdx.x == 0) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 24] = __builtin_amdgcn_s_memrealtime();
   // (the wave index through readfirstlane: wave-uniform, so the row-block addresses derived from it live in SGPRs)
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, lh = lane >> 5;
@@ -678,7 +680,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     if (rb + 1 < nrb) __syncthreads();               // the next row block's partials overwrite these
   }
   KSTAMP(7);
-  if (INFLOW_PHASE_STAMPS && pr.tbuf && threadIdx.x == 0) {
+  if (pr.tbuf && threadIdx.x == 0) {
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();
     pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 25] = __builtin_amdgcn_s_memrealtime();
     for (int v = 8; v < 16; ++v) pr.tbuf[(long)blockIdx.x * KB_TSLOTS + 8 + v] = t_;
