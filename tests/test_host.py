@@ -45,9 +45,28 @@ def test_no_process_wide_switches():
     lib = ctypes.CDLL(_hip.LIB_PATH)
     assert not hasattr(lib, 'inf_set_fused_k128') and not hasattr(lib, 'inf_set_eval_overlap')
     lib = _hip.load()
-    for opt in (_hip.INF_OPT_FUSED_K128, _hip.INF_OPT_EVAL_OVERLAP, _hip.INF_OPT_CONVERGENCE):
+    for opt in (_hip.INF_OPT_FUSED_K128, _hip.INF_OPT_EVAL_OVERLAP, _hip.INF_OPT_CONVERGENCE,
+                _hip.INF_OPT_K128_EXACT_SCALE):
         assert lib.inf_net_set_option(None, opt, 0) == -1
         assert lib.inf_net_get_option(None, opt) == -1
+
+
+def test_kernel_sources_read_no_tuning_environment():
+    """The product sources read the environment only for the per-net option defaults at inf_net_create and the host
+    wait mode (no process-wide tuning / debug switches); no #ifdef variants of the kernels."""
+    import re
+    csrc = os.path.join(os.path.dirname(_hip.__file__), '..', '..', 'csrc')
+    allowed = {'INFLOW_BLOCKING_WAIT', 'INFLOW_NO_FUSED', 'INFLOW_MFMA'}
+    names = set()
+    for f in os.listdir(csrc):
+        if not f.endswith(('.hip', '.h')):
+            continue
+        src = open(os.path.join(csrc, f)).read()
+        names |= set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', src))
+        assert not re.search(r'#\s*ifdef\s+INFLOW_', src), f
+        if f == 'engine.hip':   # the option defaults are parsed from a table of names
+            names |= {n for n in re.findall(r'"(INFLOW_[A-Z0-9_]+)"', src)}
+    assert names - allowed <= {'INFLOW_FUSED_K128', 'INFLOW_EVAL_OVERLAP', 'INFLOW_CONVERGENCE'}, names
 
 
 def test_sharded_probes_are_rows_of_the_global_draw():
