@@ -451,14 +451,18 @@ struct PsStep {
   long sb = 0, si = 0;
 };
 int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const PsStep* ps = nullptr) {
-  INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, bf.sumsq, s));
+  // fc nets write one partial per sample: with the global rule those are the sums already (0 + x == x for the
+  // non-negative or NaN sums), so the readback takes them directly and the reduction launch is skipped
+  const bool ps_on = ps && ps->on;
+  const bool direct = f->fc && !ps_on;
+  if (!direct) INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, bf.sumsq, s));
   int n = B;
-  if (ps && ps->on) {
+  if (ps_on) {
     INF_TRY(launch_ps_decide(bf.sumsq, bf.ps_state, bf.ps_active, bf.ps_improved, B, ps->k, ps->T, ps->eps, s));
     INF_TRY(launch_ps_copy(bf.ps_improved, ps->x, ps->f, bf.ps_lowx, bf.ps_lowf, B, f->d, ps->sb, ps->si, s));
     n = B + 1;
   }
-  INF_HIP(hipMemcpyAsync(sl->host, bf.sumsq, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  INF_HIP(hipMemcpyAsync(sl->host, direct ? bf.part : bf.sumsq, sizeof(double) * n, hipMemcpyDeviceToHost, s));
   INF_HIP(hipEventRecord(sl->ev, s));
   return INF_OK;
 }
@@ -562,6 +566,8 @@ bool same_shape(const InfNet* a, const InfNet* b) {
 // resid(x, gout, dg, gprev): residual g(x) -> gout (+ dg = g - gprev when gprev), per-sample partial sums of
 // squares -> bf.part, and (root solves) f(x) -> bf.fcur.  broyden_core reduces and reads them back.
 using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev)>;
+// update + residual in one launch (fused fc nets): the update ba computes ba.xnew, then the residual at it, as resid
+using StepFn = std::function<int(const BroydenArgs& ba, float* gout, float* dg, const float* gprev)>;
 
 // Copies the per-sample results (INF_CONV_PER_SAMPLE) into the stats and the caller's optional host arrays.
 static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vector<double>& lowest_ss,
@@ -599,7 +605,8 @@ static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vecto
 // sharded), with the decisions taken on the device (ps_decide_kernel) and stopped samples frozen.
 // stats.sample_* (host arrays, nullable) receive the per-sample outcome in that mode.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
-                 std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false) {
+                 std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false,
+                 const StepFn* step_fn = nullptr) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
@@ -651,9 +658,9 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   float *gx = bf.ga, *gn = bf.gb;
   float* x = xpool[0];
   float *low = per_sample ? bf.ps_lowx : x, *flow = nullptr;
+  // (U / VT need no zeroing: every update reads only the columns j < m, j < ncols that earlier steps of this solve
+  // wrote, as broyden.py:174-181 reads Us[..., :nstep - 1])
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
-  INF_HIP(hipMemsetAsync(bf.U, 0, sizeof(float) * E * T, s));
-  INF_HIP(hipMemsetAsync(bf.VT, 0, sizeof(float) * E * T, s));
   bf.fcur = fpool[0];
   INF_TRY(resid(x, gx, nullptr, nullptr));
   INF_TRY(sums(0, x, bf.fcur, slot[0]));
@@ -678,7 +685,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   int nstep = 0, lowest_step = 0;
   std::vector<double> trace{init};
   // low-rank update from iterate `step` (x = xfrom, g = gfrom) to xto (broyden.py:174-181)
-  auto update = [&](int step, float* xfrom, float* gfrom, float* xto) {
+  auto update_args = [&](int step, float* xfrom, float* gfrom, float* xto) {
     BroydenArgs ba;
     memset(&ba, 0, sizeof(ba));
     ba.batch = B;
@@ -700,7 +707,10 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     ba.m = (step - 1) % T;
     ba.ncols = std::min(step, T);
     ba.active = per_sample ? bf.ps_active : nullptr;
-    return launch_broyden_update(ba, s);
+    return ba;
+  };
+  auto update = [&](int step, float* xfrom, float* gfrom, float* xto) {
+    return launch_broyden_update(update_args(step, xfrom, gfrom, xto), s);
   };
   const bool go = per_sample ? (n_active > 0 && T > 0) : (obj >= eps && nstep < T);   // broyden.py:153
   if (go) {
@@ -715,10 +725,15 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
       float *xs = nullptr, *fs = nullptr;
       auto enqueue_next = [&](int pending_step) -> int {
         xs = pick(xpool, low, xp);
-        INF_TRY(update(pending_step, xp, gn, xs));
         fs = pick(fpool, flow, fp);
-        bf.fcur = fs;
-        INF_TRY(resid(xs, gx, bf.dg, gn));
+        if (step_fn) {
+          bf.fcur = fs;
+          INF_TRY((*step_fn)(update_args(pending_step, xp, gn, xs), gx, bf.dg, gn));
+        } else {
+          INF_TRY(update(pending_step, xp, gn, xs));
+          bf.fcur = fs;
+          INF_TRY(resid(xs, gx, bf.dg, gn));
+        }
         return sums(pending_step + 1, xs, fs, slot[1 - ps_]);
       };
       const bool spec = allow && !likely_last;
@@ -893,7 +908,27 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     }
     return eval_resid_part(f, x, x, bf.xemb, gout, dg, gprev, B, bf, s);
   };
-  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
+  // fused fc nets: each later iteration's update and residual are one launch (fcnet.hip br_on)
+  const StepFn step = [&](const BroydenArgs& ba, float* gout, float* dg, const float* gprev) {
+    OutArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in0 = bf.xemb;
+    a.in1 = ba.xnew;
+    a.in2 = gprev;
+    a.out0 = gout;
+    a.out1 = dg;
+    a.out2 = bf.fcur;
+    a.partial = bf.part;
+    a.nchunk = bf.nchunk;
+    a.mode = OM_RESID;
+    a.bias = f->L.back().b;
+    FcArgs fa = fc_args(f, ba.xnew, B);
+    fa.o = a;
+    fa.br_on = 1;
+    fa.br = ba;
+    return launch_fcnet(fa, false, s);
+  };
+  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr));
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -1761,10 +1796,23 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   int st = INF_OK;
   const float* xi = to_internal(nz, x, bf.xin, B, s, &st);
   INF_TRY(st);
-  // log|det(I + J_fx(x))| first: it depends only on x (implicit_block.py:358-362)
+  // log|det(I + J_fx(x))| first: it depends only on x (implicit_block.py:358-362).  With INF_OPT_EVAL_OVERLAP (default)
+  // it runs on the side stream beside the root solve, whose host round trips leave the GPU idle between its launches;
+  // it reads only xi (read-only below) and writes only logdet_x, and ~SideJoin joins it into s on every return path
   FcArgs fjx = fc_args(nx, xi, B);
   fjx.logdet = logdet_x;
-  INF_TRY(launch_fcnet(fjx, true, s));
+  SideJoin join;
+  if (nx->eval_overlap) {
+    SideStream* side = side_stream();
+    if (!side) return INF_ERR_HIP;
+    INF_HIP(hipEventRecord(side->fork, s));
+    INF_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+    join.side = side;
+    join.s = s;
+    INF_TRY(launch_fcnet(fjx, true, side->s));
+  } else {
+    INF_TRY(launch_fcnet(fjx, true, s));
+  }
   // x_embed = f_x(x) + x, the root solve, z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:71, 74-80, 227)
   OutArgs a;
   memset(&a, 0, sizeof(a));

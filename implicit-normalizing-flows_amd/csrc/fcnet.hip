@@ -14,12 +14,18 @@
 // output layer), fp32 accumulation: the generic path's arithmetic with another summation order.
 //
 // Layer l (M = 128 rows, K = Kpad inputs): wave w owns rows [32w, 32w + 32) and every column block.  The k index of
-// an MFMA step s is h K/2 + s for lane half h (any permutation of k shared by both operands leaves the contraction
-// unchanged), so a lane's weights are K/2 contiguous floats of its row (float4 loads straight from the engine's
-// row-major (Mpad, Kpad) packed operand, held in registers for the whole layer) and its B operand is one LDS float
-// per step and column block.  Epilogue: bias on the primal columns, the activation, and (JAC) the tangent columns
-// times act'(primal), which sits in the same lane and register of column block 0.  The output layer (d <= 16 rows)
-// splits K over the four waves (16x16x4 tiles) and sums the four partials in wave order (deterministic).
+// an MFMA step s is g K/G + s for lane group g (G = 2 groups of 32 lanes for 32x32x2 tiles, 4 of 16 for 16x16x4; any
+// permutation of k shared by both operands leaves the contraction unchanged), so a lane's weights are K/G contiguous
+// floats of its row (float4 loads straight from the engine's row-major (Mpad, Kpad) packed operand, held in registers
+// for the whole layer) and its B operand is one LDS float per step and column block.  Epilogue: bias on the primal
+// columns, the activation, and (JAC) the tangent columns times act'(primal), which sits in the same lane and register
+// of column block 0.  The output layer (d <= 16 rows) splits K over the four waves (16x16x4 tiles) and sums the four
+// partials in wave order (deterministic).
+//
+// Column-block width CW: 32 (32x32x2 tiles) for FWD; 16 (16x16x4, two row tiles per wave) for JAC, whose 16-sample
+// workgroups need 57 KiB of LDS at d = 6, so two share a CU: at POWER's B = 10 000 that is 625 workgroups on 512 slots
+// (at most 48 samples per CU) instead of 313 one-per-CU 32-sample workgroups (64 samples on the CUs that take two), and
+// each SIMD has a second wave to issue while the other waits at a barrier.
 #include <type_traits>
 
 #include "kernels.h"
@@ -31,11 +37,12 @@ constexpr int FC_H = 128;      // hidden width of the fused nets
 constexpr int FC_NT = 256;     // 4 waves
 constexpr int FC_DMAX = 16;
 
-template <int KK>
-__device__ __forceinline__ void load_wrow(const float* A, int Kpad, int row, int h, float (&w)[KK / 2]) {
-  const f32x4* p = reinterpret_cast<const f32x4*>(A + (long)row * Kpad + h * (KK / 2));
+// K / G contiguous weights of `row` for lane group g (G = 64 / CW groups)
+template <int KK, int G>
+__device__ __forceinline__ void load_wrow(const float* A, int Kpad, int row, int g, float (&w)[KK / G]) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(A + (long)row * Kpad + g * (KK / G));
 #pragma unroll
-  for (int q = 0; q < KK / 8; ++q) {
+  for (int q = 0; q < KK / G / 4; ++q) {
     const f32x4 v = p[q];
     w[4 * q] = v.x;
     w[4 * q + 1] = v.y;
@@ -45,74 +52,256 @@ __device__ __forceinline__ void load_wrow(const float* A, int Kpad, int row, int
 }
 }  // namespace
 
-// NCB column blocks of 32: FWD 32 NCB samples (one column each); JAC 32 samples x (d + 1) columns (NCB = d + 1).
-template <int NCB, bool JAC, int ACT>
+// The Broyden update of sample b (pointwise.hip broyden_small_kernel / broyden_small_d_kernel: the same sums in the
+// same order and precision) for the fused update + residual launch: x_new also goes to the net's input column
+// (in[k * ld], k < d), and to xn (the residual's zsub) with gx (its gprev) for the epilogue.
+__device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, int d, float* in, int ld,
+                                                  float (&xn)[FC_DMAX], float (&gxo)[FC_DMAX]) {
+  const long B = a.batch;
+  if (b >= B) {
+    for (int i = 0; i < d; ++i) in[i * ld] = 0.f;
+    return;
+  }
+  auto E = [&](int i) { return (long)i * a.si + b * a.sb; };
+  if (a.active && !a.active[b]) {
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      if (i >= d) continue;
+      const float x0 = a.x[E(i)];
+      a.xnew[E(i)] = x0;
+      a.dxnew[E(i)] = 0.f;
+      a.upd[E(i)] = 0.f;
+      in[i * ld] = x0;
+      xn[i] = x0;
+      gxo[i] = a.gx[E(i)];
+    }
+    return;
+  }
+  float dx[FC_DMAX], dg[FC_DMAX], vt[FC_DMAX], t[FC_DMAX];
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    dx[i] = i < d ? a.dx[E(i)] : 0.f;
+    dg[i] = i < d ? a.dg[E(i)] : 0.f;
+    vt[i] = -dx[i];
+    t[i] = -dg[i];
+  }
+#pragma unroll 2
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    float u[FC_DMAX], v[FC_DMAX];
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      u[i] = i < d ? U[E(i)] : 0.f;
+      v[i] = i < d ? V[E(i)] : 0.f;
+    }
+    double sa = 0.0, sc = 0.0;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i)
+      if (i < d) {
+        sa += (double)dx[i] * u[i];
+        sc += (double)v[i] * dg[i];
+      }
+    const float aj = (float)sa, cj = (float)sc;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      vt[i] += aj * v[i];
+      t[i] += cj * u[i];
+    }
+  }
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  float um[FC_DMAX];
+  double den = 0.0;
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    um[i] = dx[i] - t[i];
+    if (i < d) den += (double)vt[i] * dg[i];
+  }
+  const float denf = (float)den;
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    float u = um[i] / denf;
+    if (vt[i] != vt[i]) vt[i] = 0.f;
+    if (u != u) u = 0.f;
+    um[i] = u;
+    if (i < d) {
+      Vm[E(i)] = vt[i];
+      Um[E(i)] = u;
+    }
+  }
+  float gx[FC_DMAX], tt[FC_DMAX];
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    gx[i] = i < d ? a.gx[E(i)] : 0.f;
+    tt[i] = -gx[i];
+  }
+#pragma unroll 2
+  for (int j = 0; j < a.ncols; ++j) {
+    float u[FC_DMAX], v[FC_DMAX];
+    if (j == a.m) {
+#pragma unroll
+      for (int i = 0; i < FC_DMAX; ++i) {
+        u[i] = um[i];
+        v[i] = vt[i];
+      }
+    } else {
+      const float* U = a.U + (long)j * a.cs;
+      const float* V = a.VT + (long)j * a.cs;
+#pragma unroll
+      for (int i = 0; i < FC_DMAX; ++i) {
+        u[i] = i < d ? U[E(i)] : 0.f;
+        v[i] = i < d ? V[E(i)] : 0.f;
+      }
+    }
+    double se = 0.0;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i)
+      if (i < d) se += (double)v[i] * gx[i];
+    const float ej = (float)se;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) tt[i] += ej * u[i];
+  }
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    if (i >= d) continue;
+    const float up = -tt[i];
+    a.upd[E(i)] = up;
+    const float x0 = a.x[E(i)];
+    const float xe = x0 + up;
+    a.xnew[E(i)] = xe;
+    a.dxnew[E(i)] = xe - x0;
+    in[i * ld] = xe;
+    xn[i] = xe;
+    gxo[i] = gx[i];
+  }
+}
+
+// NCB column blocks of CW columns: FWD CW NCB samples (one column each); JAC CW samples x (d + 1) columns (NCB = d + 1).
+template <int NCB, bool JAC, int ACT, int CW>
 __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
-  constexpr int NC = 32 * NCB;
-  constexpr int S = JAC ? 32 : NC;
+  constexpr int NC = CW * NCB;
+  constexpr int S = JAC ? CW : NC;
+  constexpr int G = 64 / CW;                           // lane groups (k slices) per MFMA step
+  constexpr int RT = 32 / CW;                          // row tiles per wave (32 rows)
   __shared__ __attribute__((aligned(16))) float act[FC_H * NC];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, h = lane >> 5;
+  const int li = lane % CW, g = lane / CW;
   const int B = a.B, d = a.d;
   const long b0 = (long)blockIdx.x * S;
 
-  // ---- input rows [0, 16): x (primal), e_j (JAC tangent block j)
+  const bool br_on = !JAC && a.br_on;
+  // ---- input rows [0, 16): x (primal), e_j (JAC tangent block j); with br_on rows [0, d) come from the update below
   for (int i = tid; i < 16 * NC; i += FC_NT) {
     const int k = i / NC, c = i - k * NC;
-    const int cb = c >> 5, sl = JAC ? (c & 31) : c;
+    const int cb = c / CW, sl = JAC ? (c % CW) : c;
     const long b = b0 + sl;
+    if (br_on && k < d) continue;
     float v = 0.f;
     if (k < d && b < B) v = (JAC && cb > 0) ? (k == cb - 1 ? 1.f : 0.f) : a.x[(long)k * B + b];
     act[k * NC + c] = v;
+  }
+  // FWD: the epilogue's inputs (fc_out's in0 / in1 / in2 of this thread's sample) are requested now, so their latency
+  // hides under the layers (each element is read and written by the same thread only: in-place aliasing is safe)
+  float e0[JAC ? 1 : FC_DMAX], e1[JAC ? 1 : FC_DMAX], e2[JAC ? 1 : FC_DMAX];
+  if constexpr (!JAC) {
+    const OutArgs& o2 = a.o;
+    const bool mine = tid < S && b0 + tid < B;
+    const long b = b0 + tid;
+#pragma unroll
+    for (int c = 0; c < FC_DMAX; ++c) {
+      e0[c] = (mine && c < d && o2.in0) ? o2.in0[(long)c * B + b] : 0.f;
+      e1[c] = (mine && c < d && o2.in1 && !br_on) ? o2.in1[(long)c * B + b] : 0.f;
+      e2[c] = (mine && c < d && o2.in2 && !br_on) ? o2.in2[(long)c * B + b] : 0.f;
+    }
+    if (br_on && tid < S) broyden_update_fc(a.br, b0 + tid, d, act + tid, NC, e1, e2);
   }
   __syncthreads();
 
   // ---- the 128-row layers.  A layer's weights are requested while the previous layer computes (its MFMA loop
   // covers their L2 latency); each wave holds its 32 rows' weights in registers for the whole layer.
   const int row0 = 32 * w;
-  auto layer = [&](auto kc, int l, const float (&wr)[decltype(kc)::value / 2]) {
+  // accumulator register r of row tile t holds row row0 + CW t + rowoff(r): 32x32 tiles 8 (r / 4) + 4 g + r % 4,
+  // 16x16 tiles 4 g + r
+  auto rowoff = [&](int r) { return CW == 32 ? 8 * (r >> 2) + 4 * g + (r & 3) : 4 * g + r; };
+  constexpr int NR = CW == 32 ? 16 : 4;                // accumulator registers per tile
+  using accT = std::conditional_t<CW == 32, f32x16, f32x4>;
+  auto layer = [&](auto kc, int l, const float (&wr)[RT][decltype(kc)::value / G]) {
     constexpr int KK = decltype(kc)::value;
     const FcLayer& L = a.L[l];
-    f32x16 acc[NCB];
+    float bias[RT][NR];                                // this lane's output rows' biases, requested up front
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+      for (int r = 0; r < NR; ++r) bias[t][r] = L.b[row0 + CW * t + rowoff(r)];
+    accT acc[RT][NCB];
 #pragma unroll
-    for (int s = 0; s < KK / 2; ++s) {
-      const float* arow = act + (h * (KK / 2) + s) * NC + li;
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[s], arow[cb * 32], acc[cb], 0, 0, 0);
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[t][cb][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KK / G; ++s) {
+      const float* arow = act + (g * (KK / G) + s) * NC + li;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const float bv = arow[cb * CW];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          if constexpr (CW == 32) acc[t][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[t][s], bv, acc[t][cb], 0, 0, 0);
+          else acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[t][s], bv, acc[t][cb], 0, 0, 0);
+        }
+      }
     }
     const float sp = (ACT == ACT_SWISH) ? softplus_f(ldc(L.beta)) : 0.f;
     __syncthreads();                                   // every wave is done reading this layer's input
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = row0 + 8 * (r >> 2) + 4 * h + (r & 3);
-      const float bias = L.b[row];
-      if constexpr (JAC) {
-        const float z = acc[0][r] + bias;
-        const float dd = act_d<ACT>(z, sp);
-        act[row * NC + li] = act_f<ACT>(z, sp);
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int cb = 1; cb < NCB; ++cb) act[row * NC + cb * 32 + li] = acc[cb][r] * dd;
-      } else {
+      for (int r = 0; r < NR; ++r) {
+        const int row = row0 + CW * t + rowoff(r);
+        if constexpr (JAC) {
+          const float z = acc[t][0][r] + bias[t][r];
+          const float dd = act_d<ACT>(z, sp);
+          act[row * NC + li] = act_f<ACT>(z, sp);
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) act[row * NC + cb * 32 + li] = act_f<ACT>(acc[cb][r] + bias, sp);
+          for (int cb = 1; cb < NCB; ++cb) act[row * NC + cb * CW + li] = acc[t][cb][r] * dd;
+        } else {
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) act[row * NC + cb * CW + li] = act_f<ACT>(acc[t][cb][r] + bias[t][r], sp);
+        }
       }
-    }
     __syncthreads();
   };
   {
-    float w0[8], wc[FC_H / 2], wn[FC_H / 2];
-    load_wrow<16>(a.L[0].A, a.L[0].Kpad, row0 + li, h, w0);
-    if (a.nl > 2) load_wrow<FC_H>(a.L[1].A, a.L[1].Kpad, row0 + li, h, wc);
+    // PREF: the next layer's weights requested during this one (one workgroup per CU); the two-per-CU JAC variant
+    // requests each layer's weights at its start instead (the co-resident workgroup covers that latency; with the
+    // prefetch registers it would not fit two waves per SIMD)
+    constexpr bool PREF = CW == 32;
+    float w0[RT][16 / G], wc[RT][FC_H / G], wn[PREF ? RT : 1][PREF ? FC_H / G : 1];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) load_wrow<16, G>(a.L[0].A, a.L[0].Kpad, row0 + CW * t + li, g, w0[t]);
+    if (PREF && a.nl > 2)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) load_wrow<FC_H, G>(a.L[1].A, a.L[1].Kpad, row0 + CW * t + li, g, wc[t]);
     layer(std::integral_constant<int, 16>(), 0, w0);
     for (int l = 1; l < a.nl - 1; ++l) {
-      if (l + 1 < a.nl - 1) load_wrow<FC_H>(a.L[l + 1].A, a.L[l + 1].Kpad, row0 + li, h, wn);
-      layer(std::integral_constant<int, FC_H>(), l, wc);
+      if constexpr (PREF) {
+        if (l + 1 < a.nl - 1)
 #pragma unroll
-      for (int i = 0; i < FC_H / 2; ++i) wc[i] = wn[i];
+          for (int t = 0; t < RT; ++t) load_wrow<FC_H, G>(a.L[l + 1].A, a.L[l + 1].Kpad, row0 + CW * t + li, g, wn[t]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) load_wrow<FC_H, G>(a.L[l].A, a.L[l].Kpad, row0 + CW * t + li, g, wc[t]);
+      }
+      layer(std::integral_constant<int, FC_H>(), l, wc);
+      if constexpr (PREF) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < FC_H / G; ++i) wc[t][i] = wn[t][i];
+      }
     }
   }
 
@@ -159,7 +348,9 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
       const OutArgs& o2 = a.o;
       const long b = b0 + tid;
       double accd = 0.0;
-      for (int c = 0; c < d; ++c) {
+#pragma unroll
+      for (int c = 0; c < FC_DMAX; ++c) {
+        if (c >= d) continue;
         const long ei = (long)c * B + b;
         const float sv = fsum(c, tid);
         switch (o2.mode) {
@@ -167,19 +358,19 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
           case OM_EMBED: {
             const float v = sv + bias[c];
             o2.out0[ei] = v;
-            o2.out1[ei] = v + o2.in0[ei];
+            o2.out1[ei] = v + e0[c];
             break;
           }
           case OM_RESID: {
             const float v = sv + bias[c];
-            const float gx = (o2.in0[ei] - v) - o2.in1[ei];
+            const float gx = (e0[c] - v) - e1[c];
             o2.out0[ei] = gx;
-            if (o2.in2) o2.out1[ei] = gx - o2.in2[ei];
+            if (o2.in2) o2.out1[ei] = gx - e2[c];
             if (o2.out2) o2.out2[ei] = v;
             accd += (double)gx * (double)gx;
             break;
           }
-          default: o2.out0[ei] = (o2.in0[ei] - (sv + bias[c])) + o2.in1[ei]; break;   // OM_RECOMP
+          default: o2.out0[ei] = (e0[c] - (sv + bias[c])) + e1[c]; break;   // OM_RECOMP
         }
       }
       if (o2.partial) o2.partial[b] = accd;
@@ -192,7 +383,7 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
         const long ld = (long)(DM + 1) * B;
         for (int i = 0; i < DM; ++i) {
           a.tang[i * ld + b] = fsum(i, tid) + bias[i];
-          for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * 32 + tid);
+          for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * CW + tid);
         }
       }
       if (a.logdet) {
@@ -200,7 +391,7 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
 #pragma unroll
         for (int i = 0; i < DM; ++i)
 #pragma unroll
-          for (int j = 0; j < DM; ++j) M[i][j] = (i == j ? 1.f : 0.f) + fsum(i, (j + 1) * 32 + tid);
+          for (int j = 0; j < DM; ++j) M[i][j] = (i == j ? 1.f : 0.f) + fsum(i, (j + 1) * CW + tid);
         // log|det| by partial pivoting, the same order of operations as logdet_small_kernel
         float logabs = 0.f;
         int sign = 1;
@@ -250,19 +441,20 @@ int fcnet_supported(const FcArgs& a, bool jac) {
 
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s) {
   if (!fcnet_supported(a, jac)) return INF_ERR_UNSUPPORTED;
-  constexpr int FWD_NCB = 2;      // 64 samples per workgroup (32: more workgroups, measured slower)
-  const int S = jac ? 32 : 32 * FWD_NCB;
+  constexpr int FWD_NCB = 2;      // FWD: 64 samples per workgroup (32: more workgroups, measured slower)
+  constexpr int JAC_CW = 16;      // JAC: 16 samples per workgroup, two workgroups per CU
+  const int S = jac ? JAC_CW : 32 * FWD_NCB;
   const unsigned nb = (unsigned)((a.B + S - 1) / S);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define FCL(NCB_, JAC_)                                                                                         \
-  do {                                                                                                          \
-    if (a.act == ACT_SIN) hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SIN>), dim3(nb), dim3(FC_NT), 0, s, a); \
-    else hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SWISH>), dim3(nb), dim3(FC_NT), 0, s, a);               \
+#define FCL(NCB_, JAC_, CW_)                                                                                          \
+  do {                                                                                                                \
+    if (a.act == ACT_SIN) hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SIN, CW_>), dim3(nb), dim3(FC_NT), 0, s, a); \
+    else hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SWISH, CW_>), dim3(nb), dim3(FC_NT), 0, s, a);               \
   } while (0)
-  if (!jac) FCL(FWD_NCB, false);
-  else if (a.d == 2) FCL(3, true);
-  else FCL(7, true);
+  if (!jac) FCL(FWD_NCB, false, 32);
+  else if (a.d == 2) FCL(3, true, JAC_CW);
+  else FCL(7, true, JAC_CW);
 #undef FCL
   INF_CHECK_LAUNCH();
   if (prof) {

@@ -222,6 +222,11 @@ struct FcArgs {
   OutArgs o;              // FWD: fc_out's epilogue (o.Y unused: the net output stays in LDS)
   float* logdet;          // JAC (optional): log|det(I + J_f(x))| per sample
   float* tang;            // JAC (optional): (d, (d + 1) B) = [f(x) | df/dx_1 | ...], fc_jacobian's layout
+  // FWD with br_on: the Broyden update br (broyden_small_kernel's algebra, feature-major sb = 1, si = B) runs first
+  // for the workgroup's samples and its x_new is the net input (x unused); OM_RESID's in1 (= x_new) and in2 (= br.gx)
+  // then come from registers
+  int br_on;
+  BroydenArgs br;
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);

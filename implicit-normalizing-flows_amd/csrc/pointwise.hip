@@ -362,6 +362,122 @@ __global__ __launch_bounds__(256) void broyden_small_kernel(BroydenArgs a) {
   }
 }
 
+// the same update for a compile-time d (the tabular / toy nets): one pass over the old columns computes a_j, c_j and
+// folds them into vt and t as soon as they are known (the generic kernel's second pass re-reads the columns), and one
+// pass over the used columns does the same for e_j, with the new column m from registers.  Every sum runs in the same
+// order and precision as broyden_small_kernel (bit-identical); the columns' loads are independent across j, so they
+// overlap instead of forming one dependent round trip per column.
+template <int DD>
+__global__ __launch_bounds__(256) void broyden_small_d_kernel(BroydenArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.batch) return;
+  if (a.active && !a.active[b]) {
+#pragma unroll
+    for (int i = 0; i < DD; ++i) {
+      const long e = BR_IDX(b, i);
+      a.xnew[e] = a.x[e];
+      a.dxnew[e] = 0.f;
+      a.upd[e] = 0.f;
+    }
+    return;
+  }
+  float dx[DD], dg[DD], vt[DD], t[DD];
+#pragma unroll
+  for (int i = 0; i < DD; ++i) {
+    const long e = BR_IDX(b, i);
+    dx[i] = a.dx[e];
+    dg[i] = a.dg[e];
+    vt[i] = -dx[i];
+    t[i] = -dg[i];
+  }
+#pragma unroll 4
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    float u[DD], v[DD];
+    double sa = 0.0, sc = 0.0;
+#pragma unroll
+    for (int i = 0; i < DD; ++i) {
+      const long e = BR_IDX(b, i);
+      u[i] = U[e];
+      v[i] = V[e];
+    }
+#pragma unroll
+    for (int i = 0; i < DD; ++i) {
+      sa += (double)dx[i] * u[i];
+      sc += (double)v[i] * dg[i];
+    }
+    const float aj = (float)sa, cj = (float)sc;
+#pragma unroll
+    for (int i = 0; i < DD; ++i) {
+      vt[i] += aj * v[i];
+      t[i] += cj * u[i];
+    }
+  }
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  float um[DD];
+  double den = 0.0;
+#pragma unroll
+  for (int i = 0; i < DD; ++i) {
+    um[i] = dx[i] - t[i];
+    den += (double)vt[i] * dg[i];
+  }
+  const float denf = (float)den;
+#pragma unroll
+  for (int i = 0; i < DD; ++i) {
+    const long e = BR_IDX(b, i);
+    float u = um[i] / denf;
+    if (vt[i] != vt[i]) vt[i] = 0.f;
+    if (u != u) u = 0.f;
+    um[i] = u;
+    Vm[e] = vt[i];
+    Um[e] = u;
+  }
+  float gx[DD], tt[DD];
+#pragma unroll
+  for (int i = 0; i < DD; ++i) {
+    gx[i] = a.gx[BR_IDX(b, i)];
+    tt[i] = -gx[i];
+  }
+#pragma unroll 4
+  for (int j = 0; j < a.ncols; ++j) {
+    float u[DD], v[DD];
+    if (j == a.m) {
+#pragma unroll
+      for (int i = 0; i < DD; ++i) {
+        u[i] = um[i];
+        v[i] = vt[i];
+      }
+    } else {
+      const float* U = a.U + (long)j * a.cs;
+      const float* V = a.VT + (long)j * a.cs;
+#pragma unroll
+      for (int i = 0; i < DD; ++i) {
+        const long e = BR_IDX(b, i);
+        u[i] = U[e];
+        v[i] = V[e];
+      }
+    }
+    double se = 0.0;
+#pragma unroll
+    for (int i = 0; i < DD; ++i) se += (double)v[i] * gx[i];
+    const float ej = (float)se;
+#pragma unroll
+    for (int i = 0; i < DD; ++i) tt[i] += ej * u[i];
+  }
+#pragma unroll
+  for (int i = 0; i < DD; ++i) {
+    const long e = BR_IDX(b, i);
+    const float up = -tt[i];
+    a.upd[e] = up;
+    const float x0 = a.x[e];
+    const float xe = x0 + up;
+    a.xnew[e] = xe;
+    a.dxnew[e] = xe - x0;
+  }
+}
+
 // chunked multi-kernel version (large d: conv nets), grid (nchunk, B), 256 threads
 // part layout: [B][nchunk][2*T] for phase 1, [B][nchunk] (+ offset) for phase 2, [B][nchunk][T] for phase 3
 __global__ __launch_bounds__(256) void broyden_p1(BroydenArgs a, int nchunk) {
@@ -508,7 +624,11 @@ __global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, int
 int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   if (a.T > BR_TMAX || a.m >= a.T || a.ncols > a.T) return INF_ERR_INVALID;
   if (a.d <= 32) {
-    hipLaunchKernelGGL(broyden_small_kernel, dim3((a.batch + 255) / 256), dim3(256), 0, s, a);
+    const dim3 g((a.batch + 255) / 256);
+    if (a.d == 2) hipLaunchKernelGGL(broyden_small_d_kernel<2>, g, dim3(256), 0, s, a);
+    else if (a.d == 6) hipLaunchKernelGGL(broyden_small_d_kernel<6>, g, dim3(256), 0, s, a);
+    else if (a.d == 8) hipLaunchKernelGGL(broyden_small_d_kernel<8>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(broyden_small_kernel, g, dim3(256), 0, s, a);
     INF_CHECK_LAUNCH();
     return INF_OK;
   }

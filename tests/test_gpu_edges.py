@@ -256,3 +256,57 @@ def test_protective_break_banach_fallback_matches_reference(golden_dir, converge
     logpx = (logpz + lp.double().view(-1)).cpu().numpy()
     np.testing.assert_allclose(logpx, g[tag + '_logpx'], rtol=0, atol=2e-3)
     assert abs(-logpx.mean() - float(g[tag + '_nats'])) <= 1e-5
+
+
+@pytest.mark.parametrize('d', [2, 6, 7, 8])
+@pytest.mark.parametrize('nstep', [1, 3, 5])
+def test_broyden_update_small_d_matches_reference_algebra(d, nstep):
+    """The per-sample Broyden update of the small-d kernels (pointwise.hip: broyden_small_d_kernel<2 / 6 / 8>, the
+    generic broyden_small_kernel for d = 7) through inf_broyden_update, against broyden.py:174-181 restated in fp64
+    (oracle _rmatvec / _matvec).  The columns no step has written yet (j >= nstep) hold NaN: the update must not read
+    them (broyden_core no longer zeroes U / VT per solve), so the result equals the zero-filled run bit for bit."""
+    from oracle.inflow_oracle import _matvec, _rmatvec
+    lib = _hip.load()
+    B, T = 300, 5
+    m = (nstep - 1) % T
+    gen = torch.Generator().manual_seed(100 * d + nstep)
+    rnd = lambda *s: torch.randn(*s, generator=gen, dtype=torch.float64)
+    U0, VT0 = rnd(T, B, d) * 0.3, rnd(T, B, d) * 0.3
+    dx, dg, gx, x = rnd(B, d), rnd(B, d), rnd(B, d), rnd(B, d)
+    dg = dg + 2.0 * dx                                   # keeps v^T dg away from 0 for the comparison
+    U0[nstep:] = 0.0
+    VT0[nstep:] = 0.0
+
+    def run(poison):
+        U, VT = U0.float().clone(), VT0.float().clone()
+        if poison:
+            U[nstep:] = float('nan')
+            VT[nstep:] = float('nan')
+        U, VT = U.to(DEV), VT.to(DEV)
+        args = [t.float().contiguous().to(DEV) for t in (dx, dg, gx, x)]
+        upd, xn, dxn = (torch.empty(B, d, device=DEV) for _ in range(3))
+        ws = torch.empty(lib.inf_broyden_workspace_bytes(B, d, T), dtype=torch.uint8, device=DEV)
+        _hip.check(lib.inf_broyden_update(_hip.ptr(U), _hip.ptr(VT), *[_hip.ptr(t) for t in args], _hip.ptr(upd),
+                                          _hip.ptr(xn), _hip.ptr(dxn), B, d, T, nstep, _hip.ptr(ws), ws.numel(),
+                                          _hip.stream_of(U)), 'inf_broyden_update')
+        torch.cuda.synchronize()
+        return U.cpu(), VT.cpu(), upd.cpu(), xn.cpu(), dxn.cpu()
+
+    zero, pois = run(False), run(True)
+    for a, b in zip(zero[2:], pois[2:]):
+        assert torch.equal(a, b)
+    assert torch.equal(zero[0][:nstep], pois[0][:nstep]) and torch.equal(zero[1][:nstep], pois[1][:nstep])
+    # broyden.py:174-181 in fp64 on the fp32 inputs
+    f = lambda t: t.float().double()
+    Us, VTs = f(U0).permute(1, 2, 0).contiguous(), f(VT0).permute(1, 0, 2).contiguous()   # (B, d, T), (B, T, d)
+    vT = _rmatvec(Us[:, :, :m], VTs[:, :m], f(dx))
+    u = (f(dx) - _matvec(Us[:, :, :m], VTs[:, :m], f(dg))) / torch.einsum('bi, bi -> b', vT, f(dg))[:, None]
+    Us[:, :, m], VTs[:, m] = u, vT
+    update = -_matvec(Us[:, :, :nstep], VTs[:, :nstep], f(gx))
+    U, VT, upd, xn, dxn = zero
+    tol = lambda ref: dict(rtol=1e-4, atol=1e-5 * float(ref.abs().max()))
+    torch.testing.assert_close(U[m].double(), u, **tol(u))
+    torch.testing.assert_close(VT[m].double(), vT, **tol(vT))
+    torch.testing.assert_close(upd.double(), update, **tol(update))
+    torch.testing.assert_close(xn.double(), f(x) + update, **tol(update))
+    torch.testing.assert_close(dxn, xn - x.float(), rtol=0, atol=0)
