@@ -815,7 +815,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
 
 // f(0) for sample 0 of a conv net, computed once per (weights, batch size) with a B-sized launch
 static int ensure_f0(InfNet* f, int B, Bufs& bf, hipStream_t s) {
-  if (f->fc || f->f0_batch == B) return INF_OK;
+  if (f->f0_batch == B) return INF_OK;
   const size_t per = (size_t)f->d;
   if (!f->f0 && hipMalloc(&f->f0, per * sizeof(float)) != hipSuccess) return INF_ERR_HIP;
   INF_HIP(hipMemsetAsync(bf.zero, 0, sizeof(float) * per * B, s));
@@ -823,7 +823,12 @@ static int ensure_f0(InfNet* f, int B, Bufs& bf, hipStream_t s) {
   memset(&a, 0, sizeof(a));
   a.out0 = bf.fcur;
   INF_TRY(run_forward(f, bf.zero, B, bf, OM_PLAIN, &a, s));
-  INF_HIP(hipMemcpyAsync(f->f0, bf.fcur, per * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // sample 0's f(0): conv layout (B, d) row 0; fc layout (d, B) column 0
+  if (f->fc)
+    INF_HIP(hipMemcpy2DAsync(f->f0, sizeof(float), bf.fcur, sizeof(float) * (size_t)B, sizeof(float), per,
+                             hipMemcpyDeviceToDevice, s));
+  else
+    INF_HIP(hipMemcpyAsync(f->f0, bf.fcur, per * sizeof(float), hipMemcpyDeviceToDevice, s));
   f->f0_batch = B;
   return INF_OK;
 }
@@ -900,10 +905,12 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   InfBroydenStats stats = stats_for(st);
   std::vector<double> lowest_ss;
   INF_TRY(ensure_f0(f, B, bf, s));
-  bool first = !f->fc;           // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached
+  bool first = true;             // Broyden starts at z = 0 (broyden.py:136-144): f(0) is cached (per batch size, so
+                                 // that it has the bits of the batch's own kernels)
   const ResidFn resid = [&](const float* x, float* gout, float* dg, const float* gprev) {
     if (first) {
       first = false;
+      if (f->fc) return launch_resid_bcast_fc(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, s);
       return launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s);
     }
     return eval_resid_part(f, x, x, bf.xemb, gout, dg, gprev, B, bf, s);
@@ -2299,6 +2306,8 @@ int inf_net_set_option(InfNet* n, int option, int value) {
   if (value < lo || value > hi) return -INF_ERR_INVALID;
   const int prev = *slot;
   *slot = value;
+  // the kernel-variant options change the bits of f(0): the cached value is recomputed on next use
+  if (prev != value && (option == INF_OPT_FUSED_K128 || option == INF_OPT_K128_EXACT_SCALE)) n->f0_batch = -1;
   return prev;
 }
 

@@ -34,7 +34,6 @@ namespace inf {
 
 namespace {
 constexpr int FC_H = 128;      // hidden width of the fused nets
-constexpr int FC_NT = 256;     // 4 waves
 constexpr int FC_DMAX = 16;
 
 // K / G contiguous weights of `row` for lane group g (G = 64 / CW groups)
@@ -178,12 +177,16 @@ __device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, 
 }
 
 // NCB column blocks of CW columns: FWD CW NCB samples (one column each); JAC CW samples x (d + 1) columns (NCB = d + 1).
-template <int NCB, bool JAC, int ACT, int CW>
-__global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
+// NW waves, each owning FC_H / NW rows of every hidden layer.
+template <int NCB, bool JAC, int ACT, int CW, int NW>
+__global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
+  constexpr int NT = 64 * NW;
   constexpr int NC = CW * NCB;
   constexpr int S = JAC ? CW : NC;
   constexpr int G = 64 / CW;                           // lane groups (k slices) per MFMA step
-  constexpr int RT = 32 / CW;                          // row tiles per wave (32 rows)
+  constexpr int RW = FC_H / NW;                        // rows per wave
+  constexpr int RT = RW / CW;                          // row tiles per wave
+  static_assert(RT >= 1 && RW % CW == 0 && NW <= 8, "fcnet geometry");
   __shared__ __attribute__((aligned(16))) float act[FC_H * NC];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane % CW, g = lane / CW;
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
 
   const bool br_on = !JAC && a.br_on;
   // ---- input rows [0, 16): x (primal), e_j (JAC tangent block j); with br_on rows [0, d) come from the update below
-  for (int i = tid; i < 16 * NC; i += FC_NT) {
+  for (int i = tid; i < 16 * NC; i += NT) {
     const int k = i / NC, c = i - k * NC;
     const int cb = c / CW, sl = JAC ? (c % CW) : c;
     const long b = b0 + sl;
@@ -219,8 +222,8 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
   __syncthreads();
 
   // ---- the 128-row layers.  A layer's weights are requested while the previous layer computes (its MFMA loop
-  // covers their L2 latency); each wave holds its 32 rows' weights in registers for the whole layer.
-  const int row0 = 32 * w;
+  // covers their L2 latency); each wave holds its rows' weights in registers for the whole layer.
+  const int row0 = RW * w;
   // accumulator register r of row tile t holds row row0 + CW t + rowoff(r): 32x32 tiles 8 (r / 4) + 4 g + r % 4,
   // 16x16 tiles 4 g + r
   auto rowoff = [&](int r) { return CW == 32 ? 8 * (r >> 2) + 4 * g + (r & 3) : 4 * g + r; };
@@ -275,10 +278,10 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
     __syncthreads();
   };
   {
-    // PREF: the next layer's weights requested during this one (one workgroup per CU); the two-per-CU JAC variant
-    // requests each layer's weights at its start instead (the co-resident workgroup covers that latency; with the
-    // prefetch registers it would not fit two waves per SIMD)
-    constexpr bool PREF = CW == 32;
+    // PREF: the next layer's weights requested during this one (FWD); the two-per-CU JAC variant requests each
+    // layer's weights at its start instead (the co-resident workgroup covers that latency; with the prefetch
+    // registers it would not fit two waves per SIMD)
+    constexpr bool PREF = !JAC;
     float w0[RT][16 / G], wc[RT][FC_H / G], wn[PREF ? RT : 1][PREF ? FC_H / G : 1];
 #pragma unroll
     for (int t = 0; t < RT; ++t) load_wrow<16, G>(a.L[0].A, a.L[0].Kpad, row0 + CW * t + li, g, w0[t]);
@@ -305,29 +308,32 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
     }
   }
 
-  // ---- output layer: rows [0, 16) (d valid), K = 128 split over the waves (k = 32 w + 8 q + s for lane group q)
+  // ---- output layer: rows [0, 16) (d valid), K = 128 split over the waves (k = KW w + SQ q + s for lane group q)
   constexpr int NC16 = NC / 16;
+  constexpr int KW = FC_H / NW, SQ = KW / 4;
   f32x4 o[NC16];
 #pragma unroll
   for (int j = 0; j < NC16; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const FcLayer& L = a.L[a.nl - 1];
     const int q = lane >> 4, r16 = lane & 15;
-    float wr[8];
+    float wr[SQ];
     {
-      const f32x4* p = reinterpret_cast<const f32x4*>(L.A + (long)r16 * L.Kpad + 32 * w + 8 * q);
-      const f32x4 v0 = p[0], v1 = p[1];
-      wr[0] = v0.x; wr[1] = v0.y; wr[2] = v0.z; wr[3] = v0.w;
-      wr[4] = v1.x; wr[5] = v1.y; wr[6] = v1.z; wr[7] = v1.w;
+      const f32x4* p = reinterpret_cast<const f32x4*>(L.A + (long)r16 * L.Kpad + KW * w + SQ * q);
+#pragma unroll
+      for (int v = 0; v < SQ / 4; ++v) {
+        const f32x4 t = p[v];
+        wr[4 * v] = t.x; wr[4 * v + 1] = t.y; wr[4 * v + 2] = t.z; wr[4 * v + 3] = t.w;
+      }
     }
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const float* arow = act + (32 * w + 8 * q + s) * NC + r16;
+    for (int s = 0; s < SQ; ++s) {
+      const float* arow = act + (KW * w + SQ * q + s) * NC + r16;
 #pragma unroll
       for (int j = 0; j < NC16; ++j) o[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s], arow[j * 16], o[j], 0, 0, 0);
     }
   }
-  __syncthreads();                                     // act is free: the four partials go there
+  __syncthreads();                                     // act is free: the NW partials go there
   float* part = act;                                   // [wave][16 rows][NC]
   {
     const int q = lane >> 4, r16 = lane & 15;
@@ -338,7 +344,10 @@ __global__ __launch_bounds__(FC_NT) void fcnet_kernel(FcArgs a) {
   }
   __syncthreads();
   auto fsum = [&](int row, int c) {                    // the output layer's value (no bias), partials in wave order
-    return ((part[row * NC + c] + part[(16 + row) * NC + c]) + part[(32 + row) * NC + c]) + part[(48 + row) * NC + c];
+    float v = part[row * NC + c];
+#pragma unroll
+    for (int ww = 1; ww < NW; ++ww) v += part[(16 * ww + row) * NC + c];
+    return v;
   };
   const float* bias = a.L[a.nl - 1].b;
 
@@ -441,20 +450,23 @@ int fcnet_supported(const FcArgs& a, bool jac) {
 
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s) {
   if (!fcnet_supported(a, jac)) return INF_ERR_UNSUPPORTED;
-  constexpr int FWD_NCB = 2;      // FWD: 64 samples per workgroup (32: more workgroups, measured slower)
-  constexpr int JAC_CW = 16;      // JAC: 16 samples per workgroup, two workgroups per CU
-  const int S = jac ? JAC_CW : 32 * FWD_NCB;
+  // FWD: 48 samples per 8-wave workgroup (16-column blocks): 209 workgroups at B = 10 000, at most one per CU (64
+  // samples per 4-wave workgroup left 99 CUs idle and put 64 on the others); JAC: 16 samples per workgroup, two per CU
+  constexpr int FWD_NCB = 3, FWD_NW = 8;
+  constexpr int JAC_CW = 16, JAC_NW = 8;
+  const int S = jac ? JAC_CW : 16 * FWD_NCB;
   const unsigned nb = (unsigned)((a.B + S - 1) / S);
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-#define FCL(NCB_, JAC_, CW_)                                                                                          \
+#define FCL(NCB_, JAC_, CW_, NW_)                                                                                   \
   do {                                                                                                                \
-    if (a.act == ACT_SIN) hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SIN, CW_>), dim3(nb), dim3(FC_NT), 0, s, a); \
-    else hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SWISH, CW_>), dim3(nb), dim3(FC_NT), 0, s, a);               \
+    if (a.act == ACT_SIN)                                                                                             \
+      hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SIN, CW_, NW_>), dim3(nb), dim3(64 * NW_), 0, s, a);           \
+    else hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SWISH, CW_, NW_>), dim3(nb), dim3(64 * NW_), 0, s, a);      \
   } while (0)
-  if (!jac) FCL(FWD_NCB, false, 32);
-  else if (a.d == 2) FCL(3, true, JAC_CW);
-  else FCL(7, true, JAC_CW);
+  if (!jac) FCL(FWD_NCB, false, 16, FWD_NW);
+  else if (a.d == 2) FCL(3, true, JAC_CW, JAC_NW);
+  else FCL(7, true, JAC_CW, JAC_NW);
 #undef FCL
   INF_CHECK_LAUNCH();
   if (prof) {

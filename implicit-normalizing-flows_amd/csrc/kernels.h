@@ -129,6 +129,9 @@ int launch_permute_k23(const uint16_t* src, uint16_t* dst, long ntiles, hipStrea
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s);
+// fc layout (d, B): f0 holds d values
+int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
+                          int batch, int d, hipStream_t s);
 int launch_vjp_resid(const float* v, const float* y, const float* grad, const float* gprev, float* g, float* dg,
                      double* partial, int batch, int d, int nchunk, int fc, hipStream_t s);
 int launch_trace_series(const float* tang, const float* coeff, int n_terms, float* out, int d, int batch,

@@ -131,6 +131,31 @@ int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float
   return INF_OK;
 }
 
+// fc layout (d, B) of the same: one thread per sample, the sums in fc_out's / fcnet's order (bit-identical to a
+// residual evaluated at z with f(z) = f0)
+__global__ __launch_bounds__(256) void resid_bcast_fc_kernel(const float* f0, const float* xemb, const float* z, float* g,
+                                                             float* fcur, double* partial, int batch, int d) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double acc = 0.0;
+  for (int i = 0; i < d; ++i) {
+    const long e = (long)i * batch + b;
+    const float v = f0[i];
+    const float gx = (xemb[e] - v) - z[e];
+    g[e] = gx;
+    fcur[e] = v;
+    acc += (double)gx * (double)gx;
+  }
+  partial[b] = acc;
+}
+int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
+                          int batch, int d, hipStream_t s) {
+  hipLaunchKernelGGL(resid_bcast_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, f0, xemb, z, g, fcur, partial,
+                     batch, d);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // Implicit-backward residual (implicit_block.py:186-190): g = (y + v) - grad with v = y^T J (the VJP),
 // dg = g - gprev (gprev may be null), per-sample partial sums of g^2.
 // Conv layout (B, d): grid (nchunk, B), partial[b * nchunk + chunk].  fc layout (d, B): one thread per
