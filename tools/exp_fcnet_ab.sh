@@ -6,16 +6,18 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r4j}
 mkdir -p $O
 cd $R
-LIBS="base cur"
-[ -f gpurun_alt/lib_alt.so ] && LIBS="base cur alt"
+LIBS=${LIBS:-"base cur"}
+[ -f gpurun_alt/lib_alt.so ] && LIBS="$LIBS alt"
 for rep in 1 2; do
   for n in $LIBS; do
+    EV=
     case $n in
       base) L=gpurun_alt/lib_base.so ;;
+      noov) L=gpurun_alt/lib_base.so; EV=0 ;;
       alt) L=gpurun_alt/lib_alt.so ;;
       *) L= ;;
     esac
-    INFLOW_LIB=$L timeout -k 10 200 python bench.py --config power --cpu-baseline 0 --steps 10 --warmup 3 > $O/${n}_$rep.json 2>/dev/null
+    INFLOW_EVAL_OVERLAP=$EV INFLOW_LIB=$L timeout -k 10 200 python bench.py --config power --cpu-baseline 0 --steps 10 --warmup 3 > $O/${n}_$rep.json 2>/dev/null
     python -c "import json
 d=json.loads(open('$O/${n}_$rep.json').read().strip().splitlines()[-1]); print('$n', d['value'], d['ms_per_step'], d['path']['kernel_busy_frac'], [(k['kernel'], k['launches'], round(k['ms'],3)) for k in d['path']['kernels'][:3]])"
   done
@@ -28,5 +30,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --config power --cpu-baseline 0 --steps 5 --warmup 2 > $O/prof.log 2>&1
 F=$(find $O/prof -name '*kernel_stats.csv' | head -1)
 cp $F $O/kernel_stats_power.csv
+cp $(find $O/prof -name "*kernel_trace.csv" | head -1) $O/power_kernel_trace.csv
 head -4 $O/kernel_stats_power.csv | cut -c1-160
 rm -rf $O/prof
