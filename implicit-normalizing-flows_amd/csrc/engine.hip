@@ -431,7 +431,8 @@ static int sums_slot(int i, int B, SumsSlot** out) {
     if (sl.host) (void)hipHostFree(sl.host);
     sl.host = nullptr;
     const int cap = std::max(B + 1, 1024);
-    if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sizeof(double) * cap, hipHostMallocDefault) != hipSuccess)
+    // coherent: the fc residual launches write their per-sample sums straight into it (broyden_core, zero-copy)
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sizeof(double) * cap, hipHostMallocCoherent) != hipSuccess)
       return INF_ERR_HIP;
     sl.cap = cap;
   }
@@ -455,6 +456,15 @@ int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const
   // non-negative or NaN sums), so the readback takes them directly and the reduction launch is skipped
   const bool ps_on = ps && ps->on;
   const bool direct = f->fc && !ps_on;
+  if (direct && bf.part == sl->host) {               // the residual launch wrote the sums into the slot itself
+    INF_HIP(hipEventRecord(sl->ev, s));
+    return INF_OK;
+  }
+  if (!direct && !ps_on) {                            // global rule: the reduction writes the sums into the slot
+    INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, sl->host, s));
+    INF_HIP(hipEventRecord(sl->ev, s));
+    return INF_OK;
+  }
   if (!direct) INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, bf.sumsq, s));
   int n = B;
   if (ps_on) {
@@ -662,6 +672,19 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   // wrote, as broyden.py:174-181 reads Us[..., :nstep - 1])
   INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   bf.fcur = fpool[0];
+  // zero-copy readback (fc nets, global rule): each residual launch writes its per-sample sums straight into the
+  // pinned slot its norm is read from (bf.part points there while it is enqueued), so no copy launch sits between
+  // the residual and the event the host waits on; bf.part is restored on every return path
+  const bool zc = f->fc && !per_sample;
+  struct PartRestore {
+    Bufs& b;
+    double* p;
+    ~PartRestore() { b.part = p; }
+  } part_restore{bf, bf.part};
+  auto target = [&](SumsSlot* sl) {
+    if (zc) bf.part = sl->host;
+  };
+  target(slot[0]);
   INF_TRY(resid(x, gx, nullptr, nullptr));
   INF_TRY(sums(0, x, bf.fcur, slot[0]));
   if (keep_f) flow = per_sample ? bf.ps_lowf : bf.fcur;
@@ -674,6 +697,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
     fp = pick(fpool, flow, bf.fcur);
     bf.fcur = fp;
+    target(slot[1]);
     INF_TRY(resid(xp, gn, bf.dg, gx));
     INF_TRY(sums(1, xp, fp, slot[1]));
   }
@@ -724,6 +748,7 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
       const bool likely_last = !per_sample && prev_obj > 0.0 && obj * (obj / prev_obj) < eps;
       float *xs = nullptr, *fs = nullptr;
       auto enqueue_next = [&](int pending_step) -> int {
+        target(slot[1 - ps_]);
         xs = pick(xpool, low, xp);
         fs = pick(fpool, flow, fp);
         if (step_fn) {
