@@ -578,6 +578,9 @@ bool same_shape(const InfNet* a, const InfNet* b) {
 using ResidFn = std::function<int(const float* x, float* gout, float* dg, const float* gprev)>;
 // update + residual in one launch (fused fc nets): the update ba computes ba.xnew, then the residual at it, as resid
 using StepFn = std::function<int(const BroydenArgs& ba, float* gout, float* dg, const float* gprev)>;
+// Broyden's start in one launch: x0 = 0, g0 = g(x0) (+ f(x0) in bf.fcur, partials in bf.part), update = -g0,
+// x1 = x0 + update, dx = x1 - x0
+using StartFn = std::function<int(float* x0, float* g0, float* upd, float* x1, float* dx)>;
 
 // Copies the per-sample results (INF_CONV_PER_SAMPLE) into the stats and the caller's optional host arrays.
 static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vector<double>& lowest_ss,
@@ -616,7 +619,7 @@ static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vecto
 // stats.sample_* (host arrays, nullable) receive the per-sample outcome in that mode.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
                  std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false,
-                 const StepFn* step_fn = nullptr) {
+                 const StepFn* step_fn = nullptr, const StartFn* start_fn = nullptr) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
@@ -670,7 +673,9 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   float *low = per_sample ? bf.ps_lowx : x, *flow = nullptr;
   // (U / VT need no zeroing: every update reads only the columns j < m, j < ncols that earlier steps of this solve
   // wrote, as broyden.py:174-181 reads Us[..., :nstep - 1])
-  INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
+  // the one-launch start (fc nets, global rule: nothing is queued between the residual and the first step)
+  const bool fused_start = start_fn && !per_sample && T > 0;
+  if (!fused_start) INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
   bf.fcur = fpool[0];
   // zero-copy readback (fc nets, global rule): each residual launch writes its per-sample sums straight into the
   // pinned slot its norm is read from (bf.part points there while it is enqueued), so no copy launch sits between
@@ -685,16 +690,23 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     if (zc) bf.part = sl->host;
   };
   target(slot[0]);
-  INF_TRY(resid(x, gx, nullptr, nullptr));
+  float* xp = nullptr;
+  float* fp = nullptr;
+  if (fused_start) {
+    xp = pick(xpool, low, x);
+    INF_TRY((*start_fn)(x, gx, bf.upd, xp, bf.dx));
+  } else {
+    INF_TRY(resid(x, gx, nullptr, nullptr));
+  }
   INF_TRY(sums(0, x, bf.fcur, slot[0]));
   if (keep_f) flow = per_sample ? bf.ps_lowf : bf.fcur;
   // iteration 1 is queued before the initial norm is read (update = -g0, x1 = x0 + update, :144)
-  float* xp = nullptr;
-  float* fp = nullptr;
   if (T > 0) {
-    xp = pick(xpool, low, x);
-    INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
-    INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
+    if (!fused_start) {
+      xp = pick(xpool, low, x);
+      INF_TRY(launch_neg(gx, bf.upd, (long)E, s));
+      INF_TRY(launch_axpy_step(x, bf.upd, xp, bf.dx, (long)E, s));
+    }
     fp = pick(fpool, flow, bf.fcur);
     bf.fcur = fp;
     target(slot[1]);
@@ -960,7 +972,12 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     fa.br = ba;
     return launch_fcnet(fa, false, s);
   };
-  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr));
+  const StartFn start = [&](float* x0, float* g0, float* upd, float* x1, float* dx) {
+    first = false;
+    return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, upd, x1, dx, B, f->d, s);
+  };
+  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
+                       f->fc ? &start : nullptr));
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -1856,14 +1873,21 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   INF_TRY(broyden_solve(nz, xi, B, T, eps, &sst, nullptr, bf, s));
   if (stats) *stats = sst;
   if (!sst.prot_break) {
-    INF_TRY(glue_recomp(bf.fx, bf.flow, xi, bf.tmp, (long)B * nx->d, s));
-  } else {
-    memset(&a, 0, sizeof(a));
-    a.in0 = bf.fx;
-    a.in1 = xi;
-    a.out0 = bf.tmp;
-    INF_TRY(run_forward(nz, bf.lowest, B, bf, OM_RECOMP, &a, s));
+    // z = (f_x(x) - f_z(z*)) + x computed in the staging of the log|det(I + J_fz(z))| launch, which also writes z in
+    // the boundary layout (the recompute and transpose launches of the path below, in one)
+    FcArgs fjz = fc_args(nz, nullptr, B);
+    fjz.logdet = logdet_z;
+    fjz.rc_fx = bf.fx;
+    fjz.rc_fz = bf.flow;
+    fjz.rc_x = xi;
+    fjz.rc_out = z;
+    return launch_fcnet(fjz, true, s);
   }
+  memset(&a, 0, sizeof(a));
+  a.in0 = bf.fx;
+  a.in1 = xi;
+  a.out0 = bf.tmp;
+  INF_TRY(run_forward(nz, bf.lowest, B, bf, OM_RECOMP, &a, s));
   // log|det(I + J_fz(z))| at the recomputed z
   FcArgs fjz = fc_args(nz, bf.tmp, B);
   fjz.logdet = logdet_z;

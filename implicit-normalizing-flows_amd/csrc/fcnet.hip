@@ -201,7 +201,17 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
     const long b = b0 + sl;
     if (br_on && k < d) continue;
     float v = 0.f;
-    if (k < d && b < B) v = (JAC && cb > 0) ? (k == cb - 1 ? 1.f : 0.f) : a.x[(long)k * B + b];
+    if (k < d && b < B) {
+      if (JAC && cb > 0) {
+        v = k == cb - 1 ? 1.f : 0.f;
+      } else if (JAC && a.rc_fx) {                     // z = (f_x(x) - f_z(z*)) + x, written out once per element
+        const long e = (long)k * B + b;
+        v = (a.rc_fx[e] - a.rc_fz[e]) + a.rc_x[e];
+        a.rc_out[b * d + k] = v;
+      } else {
+        v = a.x[(long)k * B + b];
+      }
+    }
     act[k * NC + c] = v;
   }
   // FWD: the epilogue's inputs (fc_out's in0 / in1 / in2 of this thread's sample) are requested now, so their latency

@@ -132,6 +132,9 @@ int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float
 // fc layout (d, B): f0 holds d values
 int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                           int batch, int d, hipStream_t s);
+// x0 = 0, the residual at it, update = -g0, x1 = x0 + update, dx = x1 - x0 in one launch (fc layout)
+int launch_broyden_start_fc(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
+                            float* upd, float* x1, float* dx, int batch, int d, hipStream_t s);
 int launch_vjp_resid(const float* v, const float* y, const float* grad, const float* gprev, float* g, float* dg,
                      double* partial, int batch, int d, int nchunk, int fc, hipStream_t s);
 int launch_trace_series(const float* tang, const float* coeff, int n_terms, float* out, int d, int batch,
@@ -230,6 +233,12 @@ struct FcArgs {
   // then come from registers
   int br_on;
   BroydenArgs br;
+  // JAC with rc_fx set: the input is z = (rc_fx - rc_fz) + rc_x (glue.hip recomp_kernel, (d, B) layout), also written to
+  // rc_out in the boundary layout (B, d)
+  const float* rc_fx;
+  const float* rc_fz;
+  const float* rc_x;
+  float* rc_out;
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);

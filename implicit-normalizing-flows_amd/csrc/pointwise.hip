@@ -148,6 +148,39 @@ __global__ __launch_bounds__(256) void resid_bcast_fc_kernel(const float* f0, co
   }
   partial[b] = acc;
 }
+// Broyden's start in one launch (fc layout, broyden.py:136-144 + the first line_search step): x0 = 0, g0 = x_emb - f(0)
+// (the residual above at z = 0), update = -g0, x1 = x0 + update, dx = x1 - x0 -- the arithmetic of resid_bcast_fc,
+// neg_kernel and axpy_step_kernel, element for element
+__global__ __launch_bounds__(256) void broyden_start_fc_kernel(const float* f0, const float* xemb, float* x0, float* g,
+                                                               float* fcur, double* partial, float* upd, float* x1,
+                                                               float* dx, int batch, int d) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double acc = 0.0;
+  for (int i = 0; i < d; ++i) {
+    const long e = (long)i * batch + b;
+    const float z = 0.f;
+    const float v = f0[i];
+    const float gx = (xemb[e] - v) - z;
+    x0[e] = z;
+    g[e] = gx;
+    fcur[e] = v;
+    acc += (double)gx * (double)gx;
+    const float up = -gx;
+    upd[e] = up;
+    const float xe = z + up;
+    x1[e] = xe;
+    dx[e] = xe - z;
+  }
+  partial[b] = acc;
+}
+int launch_broyden_start_fc(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
+                            float* upd, float* x1, float* dx, int batch, int d, hipStream_t s) {
+  hipLaunchKernelGGL(broyden_start_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, f0, xemb, x0, g, fcur,
+                     partial, upd, x1, dx, batch, d);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
 int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                           int batch, int d, hipStream_t s) {
   hipLaunchKernelGGL(resid_bcast_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, f0, xemb, z, g, fcur, partial,
