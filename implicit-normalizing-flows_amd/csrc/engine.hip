@@ -1845,30 +1845,19 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   int st = INF_OK;
   const float* xi = to_internal(nz, x, bf.xin, B, s, &st);
   INF_TRY(st);
-  // log|det(I + J_fx(x))| first: it depends only on x (implicit_block.py:358-362).  With INF_OPT_EVAL_OVERLAP (default)
-  // it runs on the side stream beside the root solve, whose host round trips leave the GPU idle between its launches;
-  // it reads only xi (read-only below) and writes only logdet_x, and ~SideJoin joins it into s on every return path
-  FcArgs fjx = fc_args(nx, xi, B);
-  fjx.logdet = logdet_x;
-  SideJoin join;
-  if (nx->eval_overlap) {
-    SideStream* side = side_stream();
-    if (!side) return INF_ERR_HIP;
-    INF_HIP(hipEventRecord(side->fork, s));
-    INF_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
-    join.side = side;
-    join.s = s;
-    INF_TRY(launch_fcnet(fjx, true, side->s));
-  } else {
-    INF_TRY(launch_fcnet(fjx, true, s));
-  }
-  // x_embed = f_x(x) + x, the root solve, z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:71, 74-80, 227)
+  // log|det(I + J_fx(x))| (implicit_block.py:358-362) and x_embed = f_x(x) + x (:71) in one launch: the JAC kernel's primal
+  // column is f_x(x) with the FWD kernel's bits (the same 16-column tiles, k slices and partial order), so the x_embed
+  // launch is folded into it.  (Run beside the root solve on the side stream instead, the JAC launch took every CU
+  // first and the x_embed launch waited behind it anyway)  Then the root solve and
+  // z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:74-80, 227)
   OutArgs a;
   memset(&a, 0, sizeof(a));
-  a.in0 = xi;
-  a.out0 = bf.fx;
-  a.out1 = bf.xemb;
-  INF_TRY(run_forward(nx, xi, B, bf, OM_EMBED, &a, s));
+  FcArgs fjx = fc_args(nx, xi, B);
+  fjx.logdet = logdet_x;
+  fjx.o.in0 = xi;
+  fjx.o.out0 = bf.fx;
+  fjx.o.out1 = bf.xemb;
+  INF_TRY(launch_fcnet(fjx, true, s));
   InfBroydenStats sst = stats_for(stats);
   INF_TRY(broyden_solve(nz, xi, B, T, eps, &sst, nullptr, bf, s));
   if (stats) *stats = sst;

@@ -398,6 +398,14 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
     constexpr int DM = NCB - 1;                        // d (compile-time for the instantiated nets)
     if (tid < S && b0 + tid < B) {
       const long b = b0 + tid;
+      if (a.o.out0) {                                  // the primal column as fc_out's OM_EMBED (the FWD kernel's bits:
+        for (int i = 0; i < DM; ++i) {                 // same tiles, k slices and partial order per column)
+          const long ei = (long)i * B + b;
+          const float v = fsum(i, tid) + bias[i];
+          a.o.out0[ei] = v;
+          a.o.out1[ei] = v + a.o.in0[ei];
+        }
+      }
       if (a.tang) {
         const long ld = (long)(DM + 1) * B;
         for (int i = 0; i < DM; ++i) {

@@ -225,7 +225,8 @@ struct FcArgs {
   int nl, d, B, act;      // layers, features, batch, Act of the hidden layers
   FcLayer L[FC_MAXL];
   const float* x;         // (d, B) feature-major input
-  OutArgs o;              // FWD: fc_out's epilogue (o.Y unused: the net output stays in LDS)
+  OutArgs o;              // FWD: fc_out's epilogue (o.Y unused: the net output stays in LDS); JAC: o.out0 set -> the
+                          // primal column's OM_EMBED outputs (out0 = f(x), out1 = f(x) + in0)
   float* logdet;          // JAC (optional): log|det(I + J_f(x))| per sample
   float* tang;            // JAC (optional): (d, (d + 1) B) = [f(x) | df/dx_1 | ...], fc_jacobian's layout
   // FWD with br_on: the Broyden update br (broyden_small_kernel's algebra, feature-major sb = 1, si = B) runs first
