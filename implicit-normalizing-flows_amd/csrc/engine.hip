@@ -116,6 +116,10 @@ struct InfNet {
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
   // fused fc path (fcnet.hip): the whole net in one launch per evaluation (forward and forward-mode Jacobian)
   bool fcfused = false;
+  // f16x3 planes of the fused fc layers (fcnet_h3.hip, filled at refresh): layer l at fch + fch_off[l], exponent fchexp[l]
+  uint16_t* fch = nullptr;
+  int* fchexp = nullptr;
+  std::vector<size_t> fch_off;
 };
 
 namespace {
@@ -284,8 +288,11 @@ FcArgs fc_args(const InfNet* n, const float* x, int B) {
   f.d = n->d;
   f.B = B;
   f.act = n->L[0].act;
+  const bool h3 = n->mfma_mode == INF_MFMA_F16X3 && n->fch;
   for (int l = 0; l < f.nl && l < FC_MAXL; ++l) {
     f.L[l].A = n->L[l].f.A;
+    f.L[l].Ah = h3 ? n->fch + n->fch_off[l] : nullptr;
+    f.L[l].Aexp = h3 ? n->fchexp + l : nullptr;
     f.L[l].Kpad = n->L[l].f.Kpad;
     f.L[l].b = n->L[l].b;
     f.L[l].beta = n->L[l].act_beta;
@@ -1320,6 +1327,35 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
       for (int l = 0; l < L; ++l) f.L[l].Kpad = n->L[l].f.Kpad;
       n->fcfused = fcnet_supported(f, false) != 0;
     }
+    if (n->fcfused) {
+      // f16x3 planes (fcnet_h3.hip): the input layer 8 row tiles x 1 k step, hidden 8 x 4, output 1 x 4; fragment tiles
+      // of 2 x 512 halves.  The fused fc kernels default to f16x3 (INFLOW_MFMA=f32 / fp32: exact fp32 MFMA; the fc
+      // kernels have no bf16x6 variant, bf16x6 selects exact fp32 for them)
+      size_t halves = 0;
+      for (int l = 0; l < L; ++l) {
+        n->fch_off.push_back(halves);
+        const int nrt = l == L - 1 ? 1 : 8, nks = l == 0 ? 1 : 4;
+        halves += (size_t)nrt * nks * 1024;
+      }
+      if (hipMalloc(&n->fch, halves * sizeof(uint16_t)) != hipSuccess ||
+          hipMalloc(&n->fchexp, (size_t)L * sizeof(int)) != hipSuccess) {
+        if (n->fch) (void)hipFree(n->fch);
+        delete n;
+        return INF_ERR_HIP;
+      }
+      n->mfma_mode = INF_MFMA_F16X3;
+      const char* mm = getenv("INFLOW_MFMA");
+      if (mm && *mm) {
+        if (!strcmp(mm, "f32") || !strcmp(mm, "fp32") || !strcmp(mm, "bf16x6")) n->mfma_mode = INF_MFMA_F32;
+        else if (strcmp(mm, "f16x3") != 0) {
+          fprintf(stderr, "libinflow: INFLOW_MFMA=%s is not one of f32, fp32, bf16x6, f16x3\n", mm);
+          (void)hipFree(n->fch);
+          (void)hipFree(n->fchexp);
+          delete n;
+          return INF_ERR_INVALID;
+        }
+      }
+    }
   }
   // fused 3-1-3 conv net (run_cifar10.sh nets): 3x3 C->H, swish, 1x1 H->H, swish, 3x3 H->C
   {
@@ -1438,6 +1474,8 @@ int inf_net_destroy(InfNet* n) {
   if (n->dev) (void)hipFree(n->dev);
   if (n->scratch) (void)hipFree(n->scratch);
   if (n->f0) (void)hipFree(n->f0);
+  if (n->fch) (void)hipFree(n->fch);
+  if (n->fchexp) (void)hipFree(n->fchexp);
   delete n;
   return INF_OK;
 }
@@ -1452,6 +1490,14 @@ int inf_net_refresh(InfNet* n, void* stream) {
                          reinterpret_cast<float*>(n->scratch), s));
     INF_TRY(launch_pack(w.W, w.factor, w.f.A, w.cout, w.cin, w.ks, w.f.Mpad, w.f.Kpad, w.f.pack, s));
     INF_TRY(launch_pack(w.W, w.factor, w.g.A, w.cout, w.cin, w.ks, w.g.Mpad, w.g.Kpad, w.g.pack, s));
+  }
+  if (n->fch) {
+    const int L = (int)n->L.size();
+    for (int l = 0; l < L; ++l) {
+      const WLayer& w = n->L[l];
+      const int nrt = l == L - 1 ? 1 : 8, nks = l == 0 ? 1 : 4;
+      INF_TRY(launch_fc_split_h3(w.f.A, w.cout, w.f.Kpad, nrt, nks, n->fch + n->fch_off[l], n->fchexp + l, s));
+    }
   }
   if (n->fused) {
     const WLayer &l0 = n->L[0], &l1 = n->L[1], &l2 = n->L[2];

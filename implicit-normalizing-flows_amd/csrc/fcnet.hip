@@ -28,13 +28,11 @@
 // each SIMD has a second wave to issue while the other waits at a barrier.
 #include <type_traits>
 
-#include "kernels.h"
+#include "fcnet_common.h"
 
 namespace inf {
 
 namespace {
-constexpr int FC_H = 128;      // hidden width of the fused nets
-constexpr int FC_DMAX = 16;
 
 // K / G contiguous weights of `row` for lane group g (G = 64 / CW groups)
 template <int KK, int G>
@@ -50,131 +48,6 @@ __device__ __forceinline__ void load_wrow(const float* A, int Kpad, int row, int
   }
 }
 }  // namespace
-
-// The Broyden update of sample b (pointwise.hip broyden_small_kernel / broyden_small_d_kernel: the same sums in the
-// same order and precision) for the fused update + residual launch: x_new also goes to the net's input column
-// (in[k * ld], k < d), and to xn (the residual's zsub) with gx (its gprev) for the epilogue.
-__device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, int d, float* in, int ld,
-                                                  float (&xn)[FC_DMAX], float (&gxo)[FC_DMAX]) {
-  const long B = a.batch;
-  if (b >= B) {
-    for (int i = 0; i < d; ++i) in[i * ld] = 0.f;
-    return;
-  }
-  auto E = [&](int i) { return (long)i * a.si + b * a.sb; };
-  if (a.active && !a.active[b]) {
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
-      if (i >= d) continue;
-      const float x0 = a.x[E(i)];
-      a.xnew[E(i)] = x0;
-      a.dxnew[E(i)] = 0.f;
-      a.upd[E(i)] = 0.f;
-      in[i * ld] = x0;
-      xn[i] = x0;
-      gxo[i] = a.gx[E(i)];
-    }
-    return;
-  }
-  float dx[FC_DMAX], dg[FC_DMAX], vt[FC_DMAX], t[FC_DMAX];
-#pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
-    dx[i] = i < d ? a.dx[E(i)] : 0.f;
-    dg[i] = i < d ? a.dg[E(i)] : 0.f;
-    vt[i] = -dx[i];
-    t[i] = -dg[i];
-  }
-#pragma unroll 2
-  for (int j = 0; j < a.m; ++j) {
-    const float* U = a.U + (long)j * a.cs;
-    const float* V = a.VT + (long)j * a.cs;
-    float u[FC_DMAX], v[FC_DMAX];
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
-      u[i] = i < d ? U[E(i)] : 0.f;
-      v[i] = i < d ? V[E(i)] : 0.f;
-    }
-    double sa = 0.0, sc = 0.0;
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i)
-      if (i < d) {
-        sa += (double)dx[i] * u[i];
-        sc += (double)v[i] * dg[i];
-      }
-    const float aj = (float)sa, cj = (float)sc;
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
-      vt[i] += aj * v[i];
-      t[i] += cj * u[i];
-    }
-  }
-  float* Um = a.U + (long)a.m * a.cs;
-  float* Vm = a.VT + (long)a.m * a.cs;
-  float um[FC_DMAX];
-  double den = 0.0;
-#pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
-    um[i] = dx[i] - t[i];
-    if (i < d) den += (double)vt[i] * dg[i];
-  }
-  const float denf = (float)den;
-#pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
-    float u = um[i] / denf;
-    if (vt[i] != vt[i]) vt[i] = 0.f;
-    if (u != u) u = 0.f;
-    um[i] = u;
-    if (i < d) {
-      Vm[E(i)] = vt[i];
-      Um[E(i)] = u;
-    }
-  }
-  float gx[FC_DMAX], tt[FC_DMAX];
-#pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
-    gx[i] = i < d ? a.gx[E(i)] : 0.f;
-    tt[i] = -gx[i];
-  }
-#pragma unroll 2
-  for (int j = 0; j < a.ncols; ++j) {
-    float u[FC_DMAX], v[FC_DMAX];
-    if (j == a.m) {
-#pragma unroll
-      for (int i = 0; i < FC_DMAX; ++i) {
-        u[i] = um[i];
-        v[i] = vt[i];
-      }
-    } else {
-      const float* U = a.U + (long)j * a.cs;
-      const float* V = a.VT + (long)j * a.cs;
-#pragma unroll
-      for (int i = 0; i < FC_DMAX; ++i) {
-        u[i] = i < d ? U[E(i)] : 0.f;
-        v[i] = i < d ? V[E(i)] : 0.f;
-      }
-    }
-    double se = 0.0;
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i)
-      if (i < d) se += (double)v[i] * gx[i];
-    const float ej = (float)se;
-#pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) tt[i] += ej * u[i];
-  }
-#pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
-    if (i >= d) continue;
-    const float up = -tt[i];
-    a.upd[E(i)] = up;
-    const float x0 = a.x[E(i)];
-    const float xe = x0 + up;
-    a.xnew[E(i)] = xe;
-    a.dxnew[E(i)] = xe - x0;
-    in[i * ld] = xe;
-    xn[i] = xe;
-    gxo[i] = gx[i];
-  }
-}
 
 // NCB column blocks of CW columns: FWD CW NCB samples (one column each); JAC CW samples x (d + 1) columns (NCB = d + 1).
 // NW waves, each owning FC_H / NW rows of every hidden layer.
@@ -413,43 +286,7 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
           for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * CW + tid);
         }
       }
-      if (a.logdet) {
-        float M[DM][DM];
-#pragma unroll
-        for (int i = 0; i < DM; ++i)
-#pragma unroll
-          for (int j = 0; j < DM; ++j) M[i][j] = (i == j ? 1.f : 0.f) + fsum(i, (j + 1) * CW + tid);
-        // log|det| by partial pivoting, the same order of operations as logdet_small_kernel
-        float logabs = 0.f;
-        int sign = 1;
-#pragma unroll
-        for (int k = 0; k < DM; ++k) {
-          int piv = k;
-          float best = fabsf(M[k][k]);
-#pragma unroll
-          for (int i = k + 1; i < DM; ++i)
-            if (fabsf(M[i][k]) > best) { best = fabsf(M[i][k]); piv = i; }
-          if (piv != k) {
-#pragma unroll
-            for (int i = k + 1; i < DM; ++i)
-              if (i == piv)
-#pragma unroll
-                for (int j = 0; j < DM; ++j) { const float t = M[k][j]; M[k][j] = M[i][j]; M[i][j] = t; }
-            sign = -sign;
-          }
-          const float pv = M[k][k];
-          if (pv == 0.f) { logabs = -INFINITY; sign = 0; break; }
-          if (pv < 0.f) sign = -sign;
-          logabs += logf(fabsf(pv));
-#pragma unroll
-          for (int i = k + 1; i < DM; ++i) {
-            const float f = M[i][k] / pv;
-#pragma unroll
-            for (int j = k + 1; j < DM; ++j) M[i][j] -= f * M[k][j];
-          }
-        }
-        a.logdet[b] = sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
-      }
+      if (a.logdet) a.logdet[b] = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * CW + tid); });
     }
   }
 }
@@ -468,6 +305,7 @@ int fcnet_supported(const FcArgs& a, bool jac) {
 
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s) {
   if (!fcnet_supported(a, jac)) return INF_ERR_UNSUPPORTED;
+  const bool h3 = a.L[0].Ah != nullptr;            // scaled fp16 planes present: fcnet_h3.hip
   // FWD: 48 samples per 8-wave workgroup (16-column blocks): 209 workgroups at B = 10 000, at most one per CU (64
   // samples per 4-wave workgroup left 99 CUs idle and put 64 on the others); JAC: 16 samples per workgroup, two per CU
   constexpr int FWD_NCB = 3, FWD_NW = 8;
@@ -482,16 +320,22 @@ int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s) {
       hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SIN, CW_, NW_>), dim3(nb), dim3(64 * NW_), 0, s, a);           \
     else hipLaunchKernelGGL((fcnet_kernel<NCB_, JAC_, ACT_SWISH, CW_, NW_>), dim3(nb), dim3(64 * NW_), 0, s, a);      \
   } while (0)
-  if (!jac) FCL(FWD_NCB, false, 16, FWD_NW);
-  else if (a.d == 2) FCL(3, true, JAC_CW, JAC_NW);
-  else FCL(7, true, JAC_CW, JAC_NW);
+  if (h3) {
+    INF_TRY(launch_fcnet_h3(a, jac, s));
+  } else {
+    if (!jac) FCL(FWD_NCB, false, 16, FWD_NW);
+    else if (a.d == 2) FCL(3, true, JAC_CW, JAC_NW);
+    else FCL(7, true, JAC_CW, JAC_NW);
+    INF_CHECK_LAUNCH();
+  }
 #undef FCL
-  INF_CHECK_LAUNCH();
   if (prof) {
     const double T = jac ? a.d + 1 : 1;
     double f = 2.0 * a.d * FC_H * 2 + (double)(a.nl - 2) * 2.0 * FC_H * FC_H;   // per sample and column
     f *= T * a.B;
-    prof_end_launch(s, jac ? 601 : 600, f, 4.0 * a.B * a.d * (jac ? 2.0 : 3.0), f / PEAK_F32_FLOPS_PER_MS);
+    // MFMA instruction time at the dense peak: exact fp32 1 per algorithmic FLOP; f16x3 3 fp16 products (fcnet_h3.hip)
+    const double pk = h3 ? 3.0 * f / PEAK_BF16_FLOPS_PER_MS : f / PEAK_F32_FLOPS_PER_MS;
+    prof_end_launch(s, jac ? 601 : 600, f, 4.0 * a.B * a.d * (jac ? 2.0 : 3.0), pk);
   }
   return INF_OK;
 }

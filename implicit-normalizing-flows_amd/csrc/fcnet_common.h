@@ -1,0 +1,176 @@
+// Shared by the fused fc kernels (fcnet.hip: exact fp32 MFMA; fcnet_h3.hip: scaled two-piece fp16).
+#pragma once
+
+#include "kernels.h"
+
+namespace inf {
+
+constexpr int FC_H = 128;      // hidden width of the fused nets
+constexpr int FC_DMAX = 16;
+
+// The Broyden update of sample b (pointwise.hip broyden_small_kernel / broyden_small_d_kernel: the same sums in the
+// same order and precision) for the fused update + residual launch: x_new also goes to the net's input column
+// (in[k * ld], k < d), and to xn (the residual's zsub) with gx (its gprev) for the epilogue.
+__device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, int d, float* in, int ld,
+                                                  float (&xn)[FC_DMAX], float (&gxo)[FC_DMAX]) {
+  const long B = a.batch;
+  if (b >= B) {
+    for (int i = 0; i < d; ++i) in[i * ld] = 0.f;
+    return;
+  }
+  auto E = [&](int i) { return (long)i * a.si + b * a.sb; };
+  if (a.active && !a.active[b]) {
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      if (i >= d) continue;
+      const float x0 = a.x[E(i)];
+      a.xnew[E(i)] = x0;
+      a.dxnew[E(i)] = 0.f;
+      a.upd[E(i)] = 0.f;
+      in[i * ld] = x0;
+      xn[i] = x0;
+      gxo[i] = a.gx[E(i)];
+    }
+    return;
+  }
+  float dx[FC_DMAX], dg[FC_DMAX], vt[FC_DMAX], t[FC_DMAX];
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    dx[i] = i < d ? a.dx[E(i)] : 0.f;
+    dg[i] = i < d ? a.dg[E(i)] : 0.f;
+    vt[i] = -dx[i];
+    t[i] = -dg[i];
+  }
+#pragma unroll 2
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    float u[FC_DMAX], v[FC_DMAX];
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      u[i] = i < d ? U[E(i)] : 0.f;
+      v[i] = i < d ? V[E(i)] : 0.f;
+    }
+    double sa = 0.0, sc = 0.0;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i)
+      if (i < d) {
+        sa += (double)dx[i] * u[i];
+        sc += (double)v[i] * dg[i];
+      }
+    const float aj = (float)sa, cj = (float)sc;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) {
+      vt[i] += aj * v[i];
+      t[i] += cj * u[i];
+    }
+  }
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+  float um[FC_DMAX];
+  double den = 0.0;
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    um[i] = dx[i] - t[i];
+    if (i < d) den += (double)vt[i] * dg[i];
+  }
+  const float denf = (float)den;
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    float u = um[i] / denf;
+    if (vt[i] != vt[i]) vt[i] = 0.f;
+    if (u != u) u = 0.f;
+    um[i] = u;
+    if (i < d) {
+      Vm[E(i)] = vt[i];
+      Um[E(i)] = u;
+    }
+  }
+  float gx[FC_DMAX], tt[FC_DMAX];
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    gx[i] = i < d ? a.gx[E(i)] : 0.f;
+    tt[i] = -gx[i];
+  }
+#pragma unroll 2
+  for (int j = 0; j < a.ncols; ++j) {
+    float u[FC_DMAX], v[FC_DMAX];
+    if (j == a.m) {
+#pragma unroll
+      for (int i = 0; i < FC_DMAX; ++i) {
+        u[i] = um[i];
+        v[i] = vt[i];
+      }
+    } else {
+      const float* U = a.U + (long)j * a.cs;
+      const float* V = a.VT + (long)j * a.cs;
+#pragma unroll
+      for (int i = 0; i < FC_DMAX; ++i) {
+        u[i] = i < d ? U[E(i)] : 0.f;
+        v[i] = i < d ? V[E(i)] : 0.f;
+      }
+    }
+    double se = 0.0;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i)
+      if (i < d) se += (double)v[i] * gx[i];
+    const float ej = (float)se;
+#pragma unroll
+    for (int i = 0; i < FC_DMAX; ++i) tt[i] += ej * u[i];
+  }
+#pragma unroll
+  for (int i = 0; i < FC_DMAX; ++i) {
+    if (i >= d) continue;
+    const float up = -tt[i];
+    a.upd[E(i)] = up;
+    const float x0 = a.x[E(i)];
+    const float xe = x0 + up;
+    a.xnew[E(i)] = xe;
+    a.dxnew[E(i)] = xe - x0;
+    in[i * ld] = xe;
+    xn[i] = xe;
+    gxo[i] = gx[i];
+  }
+}
+
+// log|det(I + J)| of one sample's DM x DM Jacobian J(i, j) by partial pivoting, in logdet_small_kernel's order of
+// operations (pointwise.hip); -inf for a singular matrix, NaN for a negative determinant (torch.logdet)
+template <int DM, typename F>
+__device__ __forceinline__ float logdet_lu(F J) {
+  float M[DM][DM];
+#pragma unroll
+  for (int i = 0; i < DM; ++i)
+#pragma unroll
+    for (int j = 0; j < DM; ++j) M[i][j] = (i == j ? 1.f : 0.f) + J(i, j);
+  float logabs = 0.f;
+  int sign = 1;
+#pragma unroll
+  for (int k = 0; k < DM; ++k) {
+    int piv = k;
+    float best = fabsf(M[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < DM; ++i)
+      if (fabsf(M[i][k]) > best) { best = fabsf(M[i][k]); piv = i; }
+    if (piv != k) {
+#pragma unroll
+      for (int i = k + 1; i < DM; ++i)
+        if (i == piv)
+#pragma unroll
+          for (int j = 0; j < DM; ++j) { const float t = M[k][j]; M[k][j] = M[i][j]; M[i][j] = t; }
+      sign = -sign;
+    }
+    const float pv = M[k][k];
+    if (pv == 0.f) { logabs = -INFINITY; sign = 0; break; }
+    if (pv < 0.f) sign = -sign;
+    logabs += logf(fabsf(pv));
+#pragma unroll
+    for (int i = k + 1; i < DM; ++i) {
+      const float f = M[i][k] / pv;
+#pragma unroll
+      for (int j = k + 1; j < DM; ++j) M[i][j] -= f * M[k][j];
+    }
+  }
+  return sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
+}
+
+}  // namespace inf

@@ -1,0 +1,329 @@
+// Scaled two-piece fp16 ("f16x3", common.h) variant of the fused fc kernels (fcnet.hip): the same launches (FWD with
+// fc_out's epilogues and the optional in-kernel Broyden update; JAC with the forward-mode tangents, the LU log-det and the
+// optional recompute / x_embed), with every layer's contraction on v_mfma_f32_16x16x32_f16 instead of exact fp32 MFMA.
+//
+// Operands: each layer's weights are split once per refresh into two fp16 planes (h, l) at one power-of-two scale per
+// matrix (launch_fc_split_h3), in the 16x16x32 fragment order (lane l: row l % 16, k = 8 (l / 16) + j of a 32-wide k
+// step).  The activations live in LDS as two fp16 planes per column ([col][k], k contiguous: one ds_read_b128 per
+// plane and MFMA), each column at its own power-of-two scale (its max over the layer's rows in [2^14, 2^15)), set by
+// the producing epilogue: unscale the accumulator exactly (ldexp), bias, activation (JAC: tangents times act'), the
+// column max across the 4 lane groups (shuffles) and the 8 waves (LDS), split, write.  Three products hh + hl + lh per
+// fp32 product, fp32 accumulation: the error bound of common.h (relative to each column's and matrix's max), as on the
+// conv path.  The input rows (x, the tangent unit vectors) are split the same way (one scale per column).
+//
+// Geometry: 8 waves, wave w owns hidden rows [16 w, 16 w + 16); 16-column blocks (FWD 3 = 48 samples, JAC d + 1 for
+// 16 samples); the d-row output layer (16 padded rows) is one row tile, column block w on wave w.  K steps of 32: the
+// input layer's K = 16 is padded to 32, the hidden layers have 4 steps.  LDS at JAC d = 6: 2 planes x 112 columns x
+// 136 halves + 16 x 112 fp32 staging / output rows + the column maxima: 72 KiB, two workgroups per CU.
+#include <type_traits>
+
+#include "fcnet_common.h"
+
+namespace inf {
+
+namespace {
+constexpr int H3_NW = 8;
+constexpr int H3_NT = 64 * H3_NW;
+constexpr int H3_LD = FC_H + 8;      // halves per activation-plane column (272 B: 16-byte aligned, spreads the banks)
+
+__device__ __forceinline__ f32x4 mfma3(const u32x4 (&a)[2], const u32x4& xh, const u32x4& xl, f32x4 c) {
+  const f16x8 ah = __builtin_bit_cast(f16x8, a[0]), al = __builtin_bit_cast(f16x8, a[1]);
+  const f16x8 bh = __builtin_bit_cast(f16x8, xh), bl = __builtin_bit_cast(f16x8, xl);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+  return c;
+}
+
+// the (h, l) fragments of row tile rt, k steps [0, NKS), of a layer's planes (fragment tile (rt nks + ks): 2 x 512 halves)
+template <int NKS>
+__device__ __forceinline__ void ldw_h3(const uint16_t* A, int nks, int rt, int lane, u32x4 (&w)[NKS][2]) {
+  const u32x4* p = reinterpret_cast<const u32x4*>(A);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const long t = (long)rt * nks + ks;
+    w[ks][0] = p[(t * 2 + 0) * 64 + lane];
+    w[ks][1] = p[(t * 2 + 1) * 64 + lane];
+  }
+}
+
+// 4 fp32 values (consecutive rows of one column) -> scaled fp16 h / l pieces, packed
+__device__ __forceinline__ void split4(const float (&v)[4], float S, uint2& h, uint2& l) {
+  _Float16 hh[4], ll[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    hh[r] = (_Float16)(v[r] * S);
+    ll[r] = (_Float16)__builtin_fmaf(v[r], S, -(float)hh[r]);
+  }
+  const f16x2 a = {hh[0], hh[1]}, b = {hh[2], hh[3]}, c = {ll[0], ll[1]}, e = {ll[2], ll[3]};
+  h = make_uint2(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b));
+  l = make_uint2(__builtin_bit_cast(unsigned, c), __builtin_bit_cast(unsigned, e));
+}
+}  // namespace
+
+template <int NCB, bool JAC, int ACT>
+__global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
+  constexpr int NC = 16 * NCB;
+  constexpr int S = JAC ? 16 : NC;
+  static_assert(NCB <= H3_NW, "one output column block per wave");
+  __shared__ __attribute__((aligned(16))) uint16_t pl[2][NC * H3_LD];   // activation planes h, l: [col][k]
+  __shared__ __attribute__((aligned(16))) float tmp[16 * NC];           // input rows / output rows (fp32, [row][col])
+  __shared__ float wmax[H3_NW][NC];
+  __shared__ int sx[NC];                                                // the planes' column scale exponents
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int B = a.B, d = a.d;
+  const long b0 = (long)blockIdx.x * S;
+  const bool br_on = !JAC && a.br_on;
+
+  // ---- input rows [0, 16) in fp32: x (primal), e_j (JAC tangent block j); br_on: rows [0, d) from the update below
+  for (int i = tid; i < 16 * NC; i += H3_NT) {
+    const int k = i / NC, c = i - k * NC;
+    const int cb = c >> 4, sl = JAC ? (c & 15) : c;
+    const long b = b0 + sl;
+    if (br_on && k < d) continue;
+    float v = 0.f;
+    if (k < d && b < B) {
+      if (JAC && cb > 0) {
+        v = k == cb - 1 ? 1.f : 0.f;
+      } else if (JAC && a.rc_fx) {                     // z = (f_x(x) - f_z(z*)) + x, written out once per element
+        const long e = (long)k * B + b;
+        v = (a.rc_fx[e] - a.rc_fz[e]) + a.rc_x[e];
+        a.rc_out[b * d + k] = v;
+      } else {
+        v = a.x[(long)k * B + b];
+      }
+    }
+    tmp[k * NC + c] = v;
+  }
+  float e0[JAC ? 1 : FC_DMAX], e1[JAC ? 1 : FC_DMAX], e2[JAC ? 1 : FC_DMAX];
+  if constexpr (!JAC) {
+    const OutArgs& o2 = a.o;
+    const bool mine = tid < S && b0 + tid < B;
+    const long b = b0 + tid;
+#pragma unroll
+    for (int c = 0; c < FC_DMAX; ++c) {
+      e0[c] = (mine && c < d && o2.in0) ? o2.in0[(long)c * B + b] : 0.f;
+      e1[c] = (mine && c < d && o2.in1 && !br_on) ? o2.in1[(long)c * B + b] : 0.f;
+      e2[c] = (mine && c < d && o2.in2 && !br_on) ? o2.in2[(long)c * B + b] : 0.f;
+    }
+    if (br_on && tid < S) broyden_update_fc(a.br, b0 + tid, d, tmp + tid, NC, e1, e2);
+  }
+  // the input layer's weights (one k step) and, FWD, the first hidden layer's, requested before the barriers
+  const int nl = a.nl;
+  u32x4 w0[1][2];
+  ldw_h3<1>(a.L[0].Ah, 1, w, lane, w0);
+  __syncthreads();
+  // input planes: per column, its scale and the split of rows [0, 32) (rows >= 16 are the K padding)
+  for (int c = tid; c < NC; c += H3_NT) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m = fmaxf(m, fabsf(tmp[k * NC + c]));
+    const int e = h3_scale_exp(m);
+    const float Sc = __builtin_amdgcn_ldexpf(1.f, e);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float v = k < 16 ? tmp[k * NC + c] : 0.f;
+      const _Float16 h = (_Float16)(v * Sc);
+      const _Float16 l = (_Float16)__builtin_fmaf(v, Sc, -(float)h);
+      pl[0][c * H3_LD + k] = __builtin_bit_cast(uint16_t, h);
+      pl[1][c * H3_LD + k] = __builtin_bit_cast(uint16_t, l);
+    }
+    sx[c] = e;
+  }
+  __syncthreads();
+
+  // ---- the 128-row layers (the input layer with one k step, the hidden ones with four)
+  auto layer = [&](auto nksc, int l, const u32x4 (&wr)[decltype(nksc)::value][2]) {
+    constexpr int NKS = decltype(nksc)::value;
+    const FcLayer& L = a.L[l];
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
+    f32x4 acc[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + li;
+        const u32x4 xh = *reinterpret_cast<const u32x4*>(pl[0] + col * H3_LD + ks * 32 + 8 * g);
+        const u32x4 xl = *reinterpret_cast<const u32x4*>(pl[1] + col * H3_LD + ks * 32 + 8 * g);
+        acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
+      }
+    const int sw = ldc(L.Aexp);
+    const float sp = (ACT == ACT_SWISH) ? softplus_f(ldc(L.beta)) : 0.f;
+    float v[NCB][4];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const int e = -(sw + sx[cb * 16 + li]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (JAC) {
+        const float z = v[0][r] + bias[r];
+        const float dd = act_d<ACT>(z, sp);
+        v[0][r] = act_f<ACT>(z, sp);
+#pragma unroll
+        for (int cb = 1; cb < NCB; ++cb) v[cb][r] *= dd;
+      } else {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) v[cb][r] = act_f<ACT>(v[cb][r] + bias[r], sp);
+      }
+    }
+    // column maxima: the 4 rows of a lane, the 4 lane groups of a column (shuffles), the 8 waves (LDS)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      float m = fmaxf(fmaxf(fabsf(v[cb][0]), fabsf(v[cb][1])), fmaxf(fabsf(v[cb][2]), fabsf(v[cb][3])));
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      if (g == 0) wmax[w][cb * 16 + li] = m;
+    }
+    __syncthreads();                                   // (also: every wave is done reading this layer's input planes)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const int col = cb * 16 + li;
+      float m = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < H3_NW; ++ww) m = fmaxf(m, wmax[ww][col]);
+      const int e = h3_scale_exp(m);
+      uint2 h, lo;
+      split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
+      *reinterpret_cast<uint2*>(pl[0] + col * H3_LD + 16 * w + 4 * g) = h;
+      *reinterpret_cast<uint2*>(pl[1] + col * H3_LD + 16 * w + 4 * g) = lo;
+      if (w == 0 && g == 0) sx[col] = e;
+    }
+    __syncthreads();
+  };
+  layer(std::integral_constant<int, 1>(), 0, w0);
+  for (int l = 1; l < nl - 1; ++l) {
+    u32x4 wc[4][2];
+    ldw_h3<4>(a.L[l].Ah, 4, w, lane, wc);
+    layer(std::integral_constant<int, 4>(), l, wc);
+  }
+
+  // ---- output layer: 16 padded rows (d valid), K = 128; column block w on wave w, fp32 results to tmp [row][col]
+  if (w < NCB) {
+    const FcLayer& L = a.L[nl - 1];
+    u32x4 wo[4][2];
+    ldw_h3<4>(L.Ah, 4, 0, lane, wo);
+    const int col = w * 16 + li;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const u32x4 xh = *reinterpret_cast<const u32x4*>(pl[0] + col * H3_LD + ks * 32 + 8 * g);
+      const u32x4 xl = *reinterpret_cast<const u32x4*>(pl[1] + col * H3_LD + ks * 32 + 8 * g);
+      acc = mfma3(wo[ks], xh, xl, acc);
+    }
+    const int e = -(ldc(L.Aexp) + sx[col]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tmp[(4 * g + r) * NC + col] = __builtin_amdgcn_ldexpf(acc[r], e);
+  }
+  __syncthreads();
+  auto fsum = [&](int row, int c) { return tmp[row * NC + c]; };   // the output layer's value (no bias)
+  const float* bias = a.L[nl - 1].b;
+
+  if constexpr (!JAC) {
+    // fc_out's epilogues (pointwise.hip fc_out_kernel), one thread per sample
+    if (tid < S && b0 + tid < B) {
+      const OutArgs& o2 = a.o;
+      const long b = b0 + tid;
+      double accd = 0.0;
+#pragma unroll
+      for (int c = 0; c < FC_DMAX; ++c) {
+        if (c >= d) continue;
+        const long ei = (long)c * B + b;
+        const float sv = fsum(c, tid);
+        switch (o2.mode) {
+          case OM_PLAIN: o2.out0[ei] = sv + bias[c]; break;
+          case OM_EMBED: {
+            const float v = sv + bias[c];
+            o2.out0[ei] = v;
+            o2.out1[ei] = v + e0[c];
+            break;
+          }
+          case OM_RESID: {
+            const float v = sv + bias[c];
+            const float gx = (e0[c] - v) - e1[c];
+            o2.out0[ei] = gx;
+            if (o2.in2) o2.out1[ei] = gx - e2[c];
+            if (o2.out2) o2.out2[ei] = v;
+            accd += (double)gx * (double)gx;
+            break;
+          }
+          default: o2.out0[ei] = (e0[c] - (sv + bias[c])) + e1[c]; break;   // OM_RECOMP
+        }
+      }
+      if (o2.partial) o2.partial[b] = accd;
+    }
+  } else {
+    constexpr int DM = NCB - 1;
+    if (tid < S && b0 + tid < B) {
+      const long b = b0 + tid;
+      if (a.o.out0) {
+        for (int i = 0; i < DM; ++i) {
+          const long ei = (long)i * B + b;
+          const float v = fsum(i, tid) + bias[i];
+          a.o.out0[ei] = v;
+          a.o.out1[ei] = v + a.o.in0[ei];
+        }
+      }
+      if (a.tang) {
+        const long ld = (long)(DM + 1) * B;
+        for (int i = 0; i < DM; ++i) {
+          a.tang[i * ld + b] = fsum(i, tid) + bias[i];
+          for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * 16 + tid);
+        }
+      }
+      if (a.logdet) a.logdet[b] = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * 16 + tid); });
+    }
+  }
+}
+
+int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
+  const int S = jac ? 16 : 48;
+  const unsigned nb = (unsigned)((a.B + S - 1) / S);
+#define FCH(NCB_, JAC_)                                                                                     \
+  do {                                                                                                      \
+    if (a.act == ACT_SIN) hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SIN>), dim3(nb), dim3(H3_NT), 0, s, a); \
+    else hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SWISH>), dim3(nb), dim3(H3_NT), 0, s, a);               \
+  } while (0)
+  if (!jac) FCH(3, false);
+  else if (a.d == 2) FCH(3, true);
+  else FCH(7, true);
+#undef FCH
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+// ---- weight planes: the packed fp32 operand (Mpad, Kpad row-major) -> scaled fp16 (h, l) fragment planes ---------------
+// dst[((rt nks + ks) 2 + plane) 512 + lane 8 + j] holds row 16 rt + lane % 16, k = 32 ks + 8 (lane / 16) + j (zero past
+// M rows or Kpad columns), scale 2^exp, exp = h3_scale_exp(max |A|)
+__global__ void fc_split_h3_kernel(const float* A, int M, int Kpad, int nrt, int nks, uint16_t* dst, const int* exp) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)nrt * nks * 512;
+  if (i >= n) return;
+  const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+  const long t = i >> 9;
+  const int rt = (int)(t / nks), ks = (int)(t - (long)rt * nks);
+  const int row = 16 * rt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
+  const float x = (row < M && k < Kpad) ? A[(long)row * Kpad + k] : 0.f;
+  const float Sc = ldexpf(1.f, *exp);
+  const _Float16 h = (_Float16)(x * Sc);
+  const _Float16 l = (_Float16)__builtin_fmaf(x, Sc, -(float)h);
+  dst[(t * 2 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(uint16_t, h);
+  dst[(t * 2 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(uint16_t, l);
+}
+int launch_fc_split_h3(const float* A, int M, int Kpad, int nrt, int nks, uint16_t* dst, int* exp_out, hipStream_t s) {
+  INF_TRY(launch_amax_exp(A, (long)M * Kpad, exp_out, s));
+  const long n = (long)nrt * nks * 512;
+  hipLaunchKernelGGL(fc_split_h3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, M, Kpad, nrt, nks, dst,
+                     (const int*)exp_out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+}  // namespace inf

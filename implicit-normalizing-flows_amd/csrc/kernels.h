@@ -217,6 +217,8 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
 constexpr int FC_MAXL = 8;
 struct FcLayer {
   const float* A;         // the layer's forward operand, row-major (Mpad, Kpad) (Lipschitz-normalised W)
+  const uint16_t* Ah;     // the same as scaled fp16 (h, l) fragment planes (launch_fc_split_h3), or null: exact fp32
+  const int* Aexp;        // their scale exponent
   int Kpad;
   const float* b;         // bias
   const float* beta;      // swish beta (hidden layers of Swish nets)
@@ -243,6 +245,13 @@ struct FcArgs {
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);
+// the f16x3 kernels (fcnet_h3.hip; launch_fcnet dispatches there when a.L[0].Ah is set)
+int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s);
+// fc weight planes for the f16x3 kernels: the packed (M rows used, Kpad) fp32 operand -> nrt x nks fragment tiles of
+// 16 rows x 32 k, two scaled fp16 planes each, *exp_out = h3_scale_exp(max |A|)
+int launch_fc_split_h3(const float* A, int M, int Kpad, int nrt, int nks, uint16_t* dst, int* exp_out, hipStream_t s);
+// *exp_out = h3_scale_exp(max |src|) (pointwise.hip)
+int launch_amax_exp(const float* src, long n, int* exp_out, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------
 // parameter gradients (grad.hip)

@@ -981,12 +981,17 @@ __global__ void split2h_kernel(const float* src, uint16_t* dst, long n, const in
   dst[(tile * 2 + 0) * 512 + w] = __builtin_bit_cast(uint16_t, h);
   dst[(tile * 2 + 1) * 512 + w] = __builtin_bit_cast(uint16_t, l);
 }
-int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStream_t s) {
+int launch_amax_exp(const float* src, long n, int* exp_out, hipStream_t s) {
   INF_HIP(hipMemsetAsync(exp_out, 0, sizeof(int), s));
   const long nb = std::min<long>(256, (n + 4095) / 4096);
   hipLaunchKernelGGL(amax_part_kernel, dim3((unsigned)std::max<long>(nb, 1)), dim3(256), 0, s, src, n,
                      reinterpret_cast<unsigned*>(exp_out));
   hipLaunchKernelGGL(amax_exp_kernel, dim3(1), dim3(1), 0, s, exp_out);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+int launch_split2h(const float* src, uint16_t* dst, long n, int* exp_out, hipStream_t s) {
+  INF_TRY(launch_amax_exp(src, n, exp_out, s));
   hipLaunchKernelGGL(split2h_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, (const int*)exp_out);
   INF_CHECK_LAUNCH();
   return INF_OK;

@@ -645,15 +645,19 @@ def test_eval_overlap_matches_sequential():
     np.testing.assert_allclose(res[1][1].numpy(), res[0][1].numpy(), rtol=0, atol=2e-3)
 
 
+@pytest.mark.parametrize('mfma', ['f16x3', 'f32'])
 @pytest.mark.parametrize('arch', [syn.POWER, syn.TOY], ids=['power', 'toy'])
-def test_fused_fc_net_matches_generic(arch, monkeypatch):
-    """The fused fc kernel (fcnet.hip: the whole net per launch, fc_out's epilogues in-kernel, forward-mode Jacobian and
-    LU for the exact log-det) against the generic per-layer GEMM path (INFLOW_NO_FUSED=1 at inf_net_create) on the
-    tabular / toy density eval: the same Broyden step counts per block, nats within 1e-5, per-sample log p within 2e-4,
-    z within 2e-5; and the engine launch profile shows the fused kernels on the default path."""
+def test_fused_fc_net_matches_generic(arch, mfma, monkeypatch):
+    """The fused fc kernels (the whole net per launch, fc_out's epilogues in-kernel, forward-mode Jacobian and LU for the
+    exact log-det) against the generic per-layer GEMM path (INFLOW_NO_FUSED=1 at inf_net_create) on the tabular / toy
+    density eval, for both arithmetics of the fused kernels: f16x3 (fcnet_h3.hip, the default: scaled two-piece fp16
+    operands, three products) and exact fp32 MFMA (fcnet.hip, INFLOW_MFMA=f32).  The same Broyden step counts per block,
+    nats within 1e-5, per-sample log p within 2e-4, z within 2e-5; the engine launch profile shows the fused kernels on
+    the default path and the nets report the selected arithmetic."""
     B = 1000
     x = syn.tabular_batch(B, arch['d'], seed=17).to(DEV)
     res = {}
+    monkeypatch.setenv('INFLOW_MFMA', mfma)
     for mode in ('generic', 'fused'):
         monkeypatch.setenv('INFLOW_NO_FUSED', '1' if mode == 'generic' else '0')
         m, _ = _model(arch, B)
@@ -665,6 +669,11 @@ def test_fused_fc_net_matches_generic(arch, monkeypatch):
             stats = _hip.profile_end()
         tags = {s_['tag'] for s_ in stats}
         assert (600 in tags and 601 in tags) == (mode == 'fused'), sorted(tags)
+        if mode == 'fused':
+            want = 2 if mfma == 'f16x3' else 0
+            nets = [n for b in imblocks(m) for net in (b.nnet_x, b.nnet_z)
+                    for n in net.__dict__.get('_inf_native', {}).values()]
+            assert nets and all(n.lib.inf_net_get_mfma(n.handle) == want for n in nets)
         res[mode] = (loss.item(), logpx.view(-1).cpu().double(), z.cpu(), [b.last_broyden['nstep'] for b in imblocks(m)])
     (lg, pg, zg, ng), (lf, pf, zf, nf) = res['generic'], res['fused']
     assert ng == nf
