@@ -105,9 +105,12 @@ int inf_net_refresh(InfNet* net, void* stream);
  *                   for every element (small entries get an absolute, not a relative, bound).  Three products (lh, hl, hh) on
  *                   v_mfma_f32_32x32x16_f16, fp32 accumulation, unscaled exactly (ldexp): fp32-level error of
  *                   each dot product at twice the BF16X6 product rate, 4 instead of 6 operand bytes per weight.
+ * Fused fc nets (fcnet.hip / fcnet_h3.hip: the tabular / toy nets' whole forward or forward-mode Jacobian per launch):
+ *   INF_MFMA_F16X3 the same two-piece scaled split (weights per matrix, activations per sample column) on
+ *                  v_mfma_f32_16x16x32_f16; INF_MFMA_F32 (and BF16X6, which has no fc kernel) exact fp32 MFMA.
  * Default: INFLOW_MFMA=f32 (or fp32) / bf16x6 / f16x3 in the environment at inf_net_create, otherwise F16X3; any
  * other value makes inf_net_create fail with INF_ERR_INVALID.
- * No effect on nets outside the fused path. */
+ * No effect on nets outside the fused paths. */
 typedef enum InfMfmaMode { INF_MFMA_F32 = 0, INF_MFMA_BF16X6 = 1, INF_MFMA_F16X3 = 2 } InfMfmaMode;
 int inf_net_set_mfma(InfNet* net, int mode);
 int inf_net_get_mfma(const InfNet* net);
