@@ -109,7 +109,7 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
     }
     if (br_on && tid < S) broyden_update_fc(a.br, b0 + tid, d, tmp + tid, NC, e1, e2);
   }
-  // the input layer's weights (one k step) and, FWD, the first hidden layer's, requested before the barriers
+  // the input layer's weights (one k step), requested before the barriers
   const int nl = a.nl;
   u32x4 w0[1][2];
   ldw_h3<1>(a.L[0].Ah, 1, w, lane, w0);
@@ -198,11 +198,26 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
     }
     __syncthreads();
   };
+  // hidden layers: the next layer's weights are requested while this one runs (PREF, FWD: one workgroup per CU); the
+  // two-per-CU JAC requests each layer's at its start (its co-resident workgroup covers the latency)
+  constexpr bool PREF = !JAC;
+  u32x4 wc[4][2];
+  if (PREF && nl > 2) ldw_h3<4>(a.L[1].Ah, 4, w, lane, wc);
   layer(std::integral_constant<int, 1>(), 0, w0);
   for (int l = 1; l < nl - 1; ++l) {
-    u32x4 wc[4][2];
-    ldw_h3<4>(a.L[l].Ah, 4, w, lane, wc);
-    layer(std::integral_constant<int, 4>(), l, wc);
+    if constexpr (PREF) {
+      u32x4 wn[4][2];
+      if (l + 1 < nl - 1) ldw_h3<4>(a.L[l + 1].Ah, 4, w, lane, wn);
+      layer(std::integral_constant<int, 4>(), l, wc);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        wc[ks][0] = wn[ks][0];
+        wc[ks][1] = wn[ks][1];
+      }
+    } else {
+      ldw_h3<4>(a.L[l].Ah, 4, w, lane, wc);
+      layer(std::integral_constant<int, 4>(), l, wc);
+    }
   }
 
   // ---- output layer: 16 padded rows (d valid), K = 128; column block w on wave w, fp32 results to tmp [row][col]
