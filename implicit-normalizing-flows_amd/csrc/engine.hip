@@ -588,6 +588,14 @@ using StepFn = std::function<int(const BroydenArgs& ba, float* gout, float* dg, 
 // Broyden's start in one launch: x0 = 0, g0 = g(x0) (+ f(x0) in bf.fcur, partials in bf.part), update = -g0,
 // x1 = x0 + update, dx = x1 - x0
 using StartFn = std::function<int(float* x0, float* g0, float* upd, float* x1, float* dx)>;
+// Work that follows the solve, queued speculatively when the loop queues no further iteration (the pending one is predicted
+// to be the last, or the threshold ends the loop): fn(x, f) runs on the pending iterate and its f; x / f record what it
+// was queued for, so the caller can tell whether the solve's result (bf.lowest, bf.flow) is that iterate
+struct SpecTail {
+  std::function<int(const float* x, const float* f)> fn;
+  const float* x = nullptr;
+  const float* f = nullptr;
+};
 
 // Copies the per-sample results (INF_CONV_PER_SAMPLE) into the stats and the caller's optional host arrays.
 static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vector<double>& lowest_ss,
@@ -626,7 +634,7 @@ static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vecto
 // stats.sample_* (host arrays, nullable) receive the per-sample outcome in that mode.
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
                  std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false,
-                 const StepFn* step_fn = nullptr, const StartFn* start_fn = nullptr) {
+                 const StepFn* step_fn = nullptr, const StartFn* start_fn = nullptr, SpecTail* tail = nullptr) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
@@ -781,7 +789,13 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
         return sums(pending_step + 1, xs, fs, slot[1 - ps_]);
       };
       const bool spec = allow && !likely_last;
-      if (spec) INF_TRY(enqueue_next(nstep + 1));
+      if (spec) {
+        INF_TRY(enqueue_next(nstep + 1));
+      } else if (tail && tail->fn && !per_sample && keep_f) {
+        INF_TRY(tail->fn(xp, fp));
+        tail->x = xp;
+        tail->f = fp;
+      }
       INF_TRY(wait_sumsq(slot[ps_], B, ss, per_sample ? &n_active : nullptr));
       nstep += 1;
       x = xp;
@@ -945,7 +959,7 @@ static InfBroydenStats stats_for(const InfBroydenStats* caller) {
 }
 
 int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBroydenStats* st, float* diff_detail,
-                  Bufs& bf, hipStream_t s) {
+                  Bufs& bf, hipStream_t s, SpecTail* tail = nullptr) {
   InfBroydenStats stats = stats_for(st);
   std::vector<double> lowest_ss;
   INF_TRY(ensure_f0(f, B, bf, s));
@@ -984,7 +998,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, upd, x1, dx, B, f->d, s);
   };
   INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
-                       f->fc ? &start : nullptr));
+                       f->fc ? &start : nullptr, tail));
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -1904,19 +1918,27 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   fjx.o.out0 = bf.fx;
   fjx.o.out1 = bf.xemb;
   INF_TRY(launch_fcnet(fjx, true, s));
-  InfBroydenStats sst = stats_for(stats);
-  INF_TRY(broyden_solve(nz, xi, B, T, eps, &sst, nullptr, bf, s));
-  if (stats) *stats = sst;
-  if (!sst.prot_break) {
-    // z = (f_x(x) - f_z(z*)) + x computed in the staging of the log|det(I + J_fz(z))| launch, which also writes z in
-    // the boundary layout (the recompute and transpose launches of the path below, in one)
+  // z = (f_x(x) - f_z(z*)) + x computed in the staging of the log|det(I + J_fz(z))| launch, which also writes z in the
+  // boundary layout (the recompute and transpose launches of the path below, in one).  The solve queues it on its
+  // predicted last iterate before it reads that iterate's norm (SpecTail), so the GPU does not wait for the host's
+  // stop decision; if the solve's result is another iterate (or it breaks), it is queued again on the result.
+  auto jac_z = [&](const float* flow) {
     FcArgs fjz = fc_args(nz, nullptr, B);
     fjz.logdet = logdet_z;
     fjz.rc_fx = bf.fx;
-    fjz.rc_fz = bf.flow;
+    fjz.rc_fz = flow;
     fjz.rc_x = xi;
     fjz.rc_out = z;
     return launch_fcnet(fjz, true, s);
+  };
+  SpecTail tail;
+  tail.fn = [&](const float*, const float* f) { return jac_z(f); };
+  InfBroydenStats sst = stats_for(stats);
+  INF_TRY(broyden_solve(nz, xi, B, T, eps, &sst, nullptr, bf, s, nz->convergence == INF_CONV_GLOBAL ? &tail : nullptr));
+  if (stats) *stats = sst;
+  if (!sst.prot_break) {
+    if (tail.x && tail.x == bf.lowest && tail.f == bf.flow) return INF_OK;   // the speculative launch has the result
+    return jac_z(bf.flow);
   }
   memset(&a, 0, sizeof(a));
   a.in0 = bf.fx;

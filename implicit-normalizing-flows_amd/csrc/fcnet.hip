@@ -100,7 +100,7 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
       e1[c] = (mine && c < d && o2.in1 && !br_on) ? o2.in1[(long)c * B + b] : 0.f;
       e2[c] = (mine && c < d && o2.in2 && !br_on) ? o2.in2[(long)c * B + b] : 0.f;
     }
-    if (br_on && tid < S) broyden_update_fc(a.br, b0 + tid, d, act + tid, NC, e1, e2);
+    if (br_on && tid < S) broyden_update_fc<0>(a.br, b0 + tid, d, act + tid, NC, e1, e2);
   }
   __syncthreads();
 

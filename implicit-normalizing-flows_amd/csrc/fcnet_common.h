@@ -10,9 +10,13 @@ constexpr int FC_DMAX = 16;
 
 // The Broyden update of sample b (pointwise.hip broyden_small_kernel / broyden_small_d_kernel: the same sums in the
 // same order and precision) for the fused update + residual launch: x_new also goes to the net's input column
-// (in[k * ld], k < d), and to xn (the residual's zsub) with gx (its gprev) for the epilogue.
-__device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, int d, float* in, int ld,
+// (in[k * ld], k < d), and to xn (the residual's zsub) with gx (its gprev) for the epilogue.  DD: d at compile time
+// (0: runtime d <= FC_DMAX), so that the per-column loads of several columns fit in registers and go out together.
+template <int DD>
+__device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, int d_rt, float* in, int ld,
                                                   float (&xn)[FC_DMAX], float (&gxo)[FC_DMAX]) {
+  constexpr int N = DD ? DD : FC_DMAX;
+  const int d = DD ? DD : d_rt;
   const long B = a.batch;
   if (b >= B) {
     for (int i = 0; i < d; ++i) in[i * ld] = 0.f;
@@ -21,7 +25,7 @@ __device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, 
   auto E = [&](int i) { return (long)i * a.si + b * a.sb; };
   if (a.active && !a.active[b]) {
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
+    for (int i = 0; i < N; ++i) {
       if (i >= d) continue;
       const float x0 = a.x[E(i)];
       a.xnew[E(i)] = x0;
@@ -33,50 +37,50 @@ __device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, 
     }
     return;
   }
-  float dx[FC_DMAX], dg[FC_DMAX], vt[FC_DMAX], t[FC_DMAX];
+  float dx[N], dg[N], vt[N], t[N];
 #pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
+  for (int i = 0; i < N; ++i) {
     dx[i] = i < d ? a.dx[E(i)] : 0.f;
     dg[i] = i < d ? a.dg[E(i)] : 0.f;
     vt[i] = -dx[i];
     t[i] = -dg[i];
   }
-#pragma unroll 2
+#pragma unroll(DD ? 4 : 2)
   for (int j = 0; j < a.m; ++j) {
     const float* U = a.U + (long)j * a.cs;
     const float* V = a.VT + (long)j * a.cs;
-    float u[FC_DMAX], v[FC_DMAX];
+    float u[N], v[N];
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
+    for (int i = 0; i < N; ++i) {
       u[i] = i < d ? U[E(i)] : 0.f;
       v[i] = i < d ? V[E(i)] : 0.f;
     }
     double sa = 0.0, sc = 0.0;
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i)
+    for (int i = 0; i < N; ++i)
       if (i < d) {
         sa += (double)dx[i] * u[i];
         sc += (double)v[i] * dg[i];
       }
     const float aj = (float)sa, cj = (float)sc;
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) {
+    for (int i = 0; i < N; ++i) {
       vt[i] += aj * v[i];
       t[i] += cj * u[i];
     }
   }
   float* Um = a.U + (long)a.m * a.cs;
   float* Vm = a.VT + (long)a.m * a.cs;
-  float um[FC_DMAX];
+  float um[N];
   double den = 0.0;
 #pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
+  for (int i = 0; i < N; ++i) {
     um[i] = dx[i] - t[i];
     if (i < d) den += (double)vt[i] * dg[i];
   }
   const float denf = (float)den;
 #pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
+  for (int i = 0; i < N; ++i) {
     float u = um[i] / denf;
     if (vt[i] != vt[i]) vt[i] = 0.f;
     if (u != u) u = 0.f;
@@ -86,18 +90,18 @@ __device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, 
       Um[E(i)] = u;
     }
   }
-  float gx[FC_DMAX], tt[FC_DMAX];
+  float gx[N], tt[N];
 #pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
+  for (int i = 0; i < N; ++i) {
     gx[i] = i < d ? a.gx[E(i)] : 0.f;
     tt[i] = -gx[i];
   }
-#pragma unroll 2
+#pragma unroll(DD ? 4 : 2)
   for (int j = 0; j < a.ncols; ++j) {
-    float u[FC_DMAX], v[FC_DMAX];
+    float u[N], v[N];
     if (j == a.m) {
 #pragma unroll
-      for (int i = 0; i < FC_DMAX; ++i) {
+      for (int i = 0; i < N; ++i) {
         u[i] = um[i];
         v[i] = vt[i];
       }
@@ -105,21 +109,21 @@ __device__ __forceinline__ void broyden_update_fc(const BroydenArgs& a, long b, 
       const float* U = a.U + (long)j * a.cs;
       const float* V = a.VT + (long)j * a.cs;
 #pragma unroll
-      for (int i = 0; i < FC_DMAX; ++i) {
+      for (int i = 0; i < N; ++i) {
         u[i] = i < d ? U[E(i)] : 0.f;
         v[i] = i < d ? V[E(i)] : 0.f;
       }
     }
     double se = 0.0;
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i)
+    for (int i = 0; i < N; ++i)
       if (i < d) se += (double)v[i] * gx[i];
     const float ej = (float)se;
 #pragma unroll
-    for (int i = 0; i < FC_DMAX; ++i) tt[i] += ej * u[i];
+    for (int i = 0; i < N; ++i) tt[i] += ej * u[i];
   }
 #pragma unroll
-  for (int i = 0; i < FC_DMAX; ++i) {
+  for (int i = 0; i < N; ++i) {
     if (i >= d) continue;
     const float up = -tt[i];
     a.upd[E(i)] = up;

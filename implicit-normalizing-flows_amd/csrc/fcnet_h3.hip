@@ -61,7 +61,8 @@ __device__ __forceinline__ void split4(const float (&v)[4], float S, uint2& h, u
 }
 }  // namespace
 
-template <int NCB, bool JAC, int ACT>
+// DD: the FWD kernels' d at compile time for the in-kernel Broyden update (0: runtime)
+template <int NCB, bool JAC, int ACT, int DD>
 __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
   constexpr int NC = 16 * NCB;
   constexpr int S = JAC ? 16 : NC;
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
       e1[c] = (mine && c < d && o2.in1 && !br_on) ? o2.in1[(long)c * B + b] : 0.f;
       e2[c] = (mine && c < d && o2.in2 && !br_on) ? o2.in2[(long)c * B + b] : 0.f;
     }
-    if (br_on && tid < S) broyden_update_fc(a.br, b0 + tid, d, tmp + tid, NC, e1, e2);
+    if (br_on && tid < S) broyden_update_fc<DD>(a.br, b0 + tid, d, tmp + tid, NC, e1, e2);
   }
   // the input layer's weights (one k step), requested before the barriers
   const int nl = a.nl;
@@ -301,14 +302,22 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
 int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
   const int S = jac ? 16 : 48;
   const unsigned nb = (unsigned)((a.B + S - 1) / S);
-#define FCH(NCB_, JAC_)                                                                                     \
-  do {                                                                                                      \
-    if (a.act == ACT_SIN) hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SIN>), dim3(nb), dim3(H3_NT), 0, s, a); \
-    else hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SWISH>), dim3(nb), dim3(H3_NT), 0, s, a);               \
+#define FCH(NCB_, JAC_, DD_)                                                                                     \
+  do {                                                                                                           \
+    if (a.act == ACT_SIN)                                                                                        \
+      hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SIN, DD_>), dim3(nb), dim3(H3_NT), 0, s, a);           \
+    else hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SWISH, DD_>), dim3(nb), dim3(H3_NT), 0, s, a);      \
   } while (0)
-  if (!jac) FCH(3, false);
-  else if (a.d == 2) FCH(3, true);
-  else FCH(7, true);
+  if (!jac) {
+    if (a.d == 6) FCH(3, false, 6);
+    else if (a.d == 2) FCH(3, false, 2);
+    else if (a.d == 8) FCH(3, false, 8);
+    else FCH(3, false, 0);
+  } else if (a.d == 2) {
+    FCH(3, true, 0);
+  } else {
+    FCH(7, true, 0);
+  }
 #undef FCH
   INF_CHECK_LAUNCH();
   return INF_OK;
