@@ -1902,9 +1902,8 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   hipStream_t s = (hipStream_t)stream;
   Bufs bf;
   if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
-  int st = INF_OK;
-  const float* xi = to_internal(nz, x, bf.xin, B, s, &st);
-  INF_TRY(st);
+  // x in the internal layout: written by the x-branch JAC launch's staging (it reads x in the boundary layout)
+  const float* xi = bf.xin;
   // log|det(I + J_fx(x))| (implicit_block.py:358-362) and x_embed = f_x(x) + x (:71) in one launch: the JAC kernel's primal
   // column is f_x(x) with the FWD kernel's bits (the same 16-column tiles, k slices and partial order), so the x_embed
   // launch is folded into it.  (Run beside the root solve on the side stream instead, the JAC launch took every CU
@@ -1912,7 +1911,9 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   // z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:74-80, 227)
   OutArgs a;
   memset(&a, 0, sizeof(a));
-  FcArgs fjx = fc_args(nx, xi, B);
+  FcArgs fjx = fc_args(nx, nullptr, B);
+  fjx.x_bnd = x;
+  fjx.x_int = bf.xin;
   fjx.logdet = logdet_x;
   fjx.o.in0 = xi;
   fjx.o.out0 = bf.fx;

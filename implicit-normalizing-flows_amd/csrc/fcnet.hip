@@ -77,6 +77,9 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
     if (k < d && b < B) {
       if (JAC && cb > 0) {
         v = k == cb - 1 ? 1.f : 0.f;
+      } else if (JAC && a.x_bnd) {                     // x in the boundary layout (B, d), written out internal (d, B)
+        v = a.x_bnd[b * d + k];
+        a.x_int[(long)k * B + b] = v;
       } else if (JAC && a.rc_fx) {                     // z = (f_x(x) - f_z(z*)) + x, written out once per element
         const long e = (long)k * B + b;
         v = (a.rc_fx[e] - a.rc_fz[e]) + a.rc_x[e];
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
           const long ei = (long)i * B + b;
           const float v = fsum(i, tid) + bias[i];
           a.o.out0[ei] = v;
-          a.o.out1[ei] = v + a.o.in0[ei];
+          a.o.out1[ei] = v + (a.x_bnd ? a.x_bnd[b * DM + i] : a.o.in0[ei]);   // (x_int is this launch's output)
         }
       }
       if (a.tang) {

@@ -242,6 +242,10 @@ struct FcArgs {
   const float* rc_fz;
   const float* rc_x;
   float* rc_out;
+  // JAC with x_bnd set: the input is read in the boundary layout (B, d) and also written to x_int in the internal
+  // layout (d, B) (the transpose launch folded into the staging)
+  const float* x_bnd;
+  float* x_int;
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);
