@@ -1,31 +1,33 @@
-// Fused fc net: one launch per net evaluation of the tabular / toy nets (train_tabular.py:292-311 build_nnet,
-// train_toy.py:146-171): InducedNormLinear(d, 128), act, [InducedNormLinear(128, 128), act] x n, InducedNormLinear(128, d)
-// with act = Sin or Swish.  The generic path runs every layer as its own GEMM launch over the (d, B) feature-major
-// batch (POWER at B = 10 000: 5 launches per evaluation plus the epilogue, 5.5 TF/s, launch- and latency-bound);
-// here one workgroup carries S samples through all layers with the activations in LDS:
+// Fused fc net, exact fp32 MFMA (INF_MFMA_F32; the default f16x3 variant is fcnet_h3.hip): one launch per net evaluation
+// of the tabular / toy nets (train_tabular.py:292-311 build_nnet, train_toy.py:146-171): InducedNormLinear(d, 128), act,
+// [InducedNormLinear(128, 128), act] x n, InducedNormLinear(128, d) with act = Sin or Swish.  The generic path runs
+// every layer as its own GEMM launch over the (d, B) feature-major batch (POWER at B = 10 000: 5 launches per
+// evaluation plus the epilogue, 5.5 TF/s, launch- and latency-bound); here one workgroup carries S samples through
+// all layers with the activations in LDS:
 //
-//   FWD: f(x) for 32 NCB samples, followed in-kernel by fc_out's epilogues (x_embed, the Broyden residual and its
-//        per-sample |g|^2, the z recompute; pointwise.hip fc_out_kernel);
-//   JAC: forward-mode f and its d tangents (batch_jacobian, implicit_block.py:249-260,358-362) for 32 samples,
+//   FWD: f(x) for CW NCB samples, followed in-kernel by fc_out's epilogues (x_embed, the Broyden residual and its
+//        per-sample |g|^2, the z recompute; pointwise.hip fc_out_kernel), optionally after the Broyden update that
+//        produces its input (br_on, fcnet_common.h broyden_update_fc);
+//   JAC: forward-mode f and its d tangents (batch_jacobian, implicit_block.py:249-260,358-362) for CW samples,
 //        NCB = d + 1 column blocks [f | df/dx_1 | ... | df/dx_d], then log|det(I + J)| per sample by partial-pivot LU
-//        in registers (torch.logdet; pointwise.hip logdet_small_kernel), and / or the tangents themselves.
+//        in registers (torch.logdet; pointwise.hip logdet_small_kernel), the tangents, and / or the primal column's
+//        x_embed; the input may be the z recompute or x in the boundary layout (both written out).
 //
-// Arithmetic: exact fp32 MFMA (v_mfma_f32_32x32x2_f32 for the 128-row layers, v_mfma_f32_16x16x4_f32 for the d-row
-// output layer), fp32 accumulation: the generic path's arithmetic with another summation order.
+// Arithmetic: exact fp32 MFMA (v_mfma_f32_16x16x4_f32, or 32x32x2 for 32-column blocks), fp32 accumulation: the generic
+// path's arithmetic with another summation order.
 //
-// Layer l (M = 128 rows, K = Kpad inputs): wave w owns rows [32w, 32w + 32) and every column block.  The k index of
-// an MFMA step s is g K/G + s for lane group g (G = 2 groups of 32 lanes for 32x32x2 tiles, 4 of 16 for 16x16x4; any
-// permutation of k shared by both operands leaves the contraction unchanged), so a lane's weights are K/G contiguous
-// floats of its row (float4 loads straight from the engine's row-major (Mpad, Kpad) packed operand, held in registers
-// for the whole layer) and its B operand is one LDS float per step and column block.  Epilogue: bias on the primal
-// columns, the activation, and (JAC) the tangent columns times act'(primal), which sits in the same lane and register
-// of column block 0.  The output layer (d <= 16 rows) splits K over the four waves (16x16x4 tiles) and sums the four
+// Layer l (M = 128 rows, K = Kpad inputs): wave w owns rows [RW w, RW w + RW) (RW = 128 / NW) and every column block.
+// The k index of an MFMA step s is g K/G + s for lane group g (G = 2 groups of 32 lanes for 32x32x2 tiles, 4 of 16 for
+// 16x16x4; any permutation of k shared by both operands leaves the contraction unchanged), so a lane's weights are K/G
+// contiguous floats of its row (float4 loads straight from the engine's row-major (Mpad, Kpad) packed operand, held in
+// registers for the whole layer) and its B operand is one LDS float per step and column block.  Epilogue: bias on the
+// primal columns, the activation, and (JAC) the tangent columns times act'(primal), which sits in the same lane and
+// register of column block 0.  The output layer (d <= 16 rows) splits K over the waves (16x16x4 tiles) and sums the
 // partials in wave order (deterministic).
 //
-// Column-block width CW: 32 (32x32x2 tiles) for FWD; 16 (16x16x4, two row tiles per wave) for JAC, whose 16-sample
-// workgroups need 57 KiB of LDS at d = 6, so two share a CU: at POWER's B = 10 000 that is 625 workgroups on 512 slots
-// (at most 48 samples per CU) instead of 313 one-per-CU 32-sample workgroups (64 samples on the CUs that take two), and
-// each SIMD has a second wave to issue while the other waits at a barrier.
+// Geometry (launch_fcnet): 16-column blocks and 8 waves for both.  FWD: 48 samples per workgroup, 209 at B = 10 000,
+// one per CU (64-sample 4-wave workgroups left 99 CUs idle).  JAC: 16 samples per workgroup (57 KiB of LDS at d = 6),
+// two per CU: 625 workgroups on 512 slots (at most 48 samples per CU instead of 64 with 313 32-sample workgroups).
 #include <type_traits>
 
 #include "fcnet_common.h"
