@@ -93,6 +93,13 @@ MFMA_DESC = {
              'v_mfma_f32_32x32x16_f16, fp32 accumulation, exact unscale (error at fp32 level, '
              'tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
     'f32': 'f32: v_mfma_f32_32x32x2_f32'}
+# the fused fc kernels (tabular configs): fcnet_h3.hip / fcnet.hip
+MFMA_DESC_FC = {
+    'f16x3': 'f16x3: fp32 operands scaled by 2^s (weights per matrix, activations per sample column) and split into 2 '
+             'fp16 pieces, 3 products per fp32 product on v_mfma_f32_16x16x32_f16, fp32 accumulation, exact unscale '
+             '(tests/test_gpu_parity.py::test_fused_fc_net_matches_generic)',
+    'bf16x6': 'f32: v_mfma_f32_16x16x4_f32 (the fc kernels have no bf16x6 variant)',
+    'f32': 'f32: v_mfma_f32_16x16x4_f32'}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -368,7 +375,7 @@ def main():
         'value': round(value, 3), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
         'scaling': 'strong' if global_batch is not None else 'weak', 'vs_baseline': None, 'dtype': 'f32',
-        'mfma': MFMA_DESC[mm],
+        'mfma': (MFMA_DESC if image else MFMA_DESC_FC)[mm],
         'data': ('synthetic dequantised %s images, deterministic random-init weights (lib/synthetic.py)'
                  % 'x'.join(map(str, arch['input_size']))) if image else
                 ('synthetic standardised N(0, 1) rows (d = %d), deterministic random-init weights (lib/synthetic.py)'
@@ -387,8 +394,10 @@ def main():
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
                      'traffic_source': traffic_src,
                      'algorithmic_bytes_per_launch': dom['bytes'] / dom['launches'],
-                     'schedule': 'per-kernel durations from one extra step on the sequential eval schedule (timed '
-                                 'steps: %s)' % ('x-branch series on a side stream' if overlap_on else 'sequential'),
+                     'schedule': ('per-kernel durations from one extra step on the sequential eval schedule (timed '
+                                  'steps: %s)' % ('x-branch series on a side stream' if overlap_on else 'sequential'))
+                     if image else 'per-kernel durations from one extra step (one stream: the x-branch log-det and '
+                                   'x_embed are one launch)',
                      'flops_per_launch': dom['flops'] / dom['launches']},
         'path': {'gemm_tflops_per_step': round(total_gemm_flops / 1e12, 4),
                  'gemm_flop_rate_tflops': round(total_gemm_flops / (prof_wall * 1e12), 2),
