@@ -163,6 +163,10 @@ class InducedNormLinear(nn.Module):
             self.scale.copy_(sigma)
         return W / torch.max(torch.ones(1, device=W.device), sigma / self.coeff)
 
+    def compute_domain_codomain(self):
+        """(domain, codomain) of the induced norm (mixed_lipschitz.py:68-74); always (2, 2) here."""
+        return self.domain, self.codomain
+
     def compute_one_iter(self):
         W = self.weight.detach()
         u = _unit(torch.mv(W, self.v))
@@ -294,6 +298,10 @@ class InducedNormConv2d(nn.Module):
         with torch.no_grad():
             self.scale.copy_(sigma)
         return W / torch.max(torch.ones(1, device=W.device), sigma / self.coeff)
+
+    def compute_domain_codomain(self):
+        """(domain, codomain) of the induced norm (mixed_lipschitz.py:180-186); always (2, 2) here."""
+        return self.domain, self.codomain
 
     def compute_one_iter(self):
         if not self.initialized:

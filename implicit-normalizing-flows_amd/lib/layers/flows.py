@@ -14,7 +14,7 @@ import torch.nn as nn
 from .. import _hip
 
 __all__ = ['SequentialFlow', 'Inverse', 'SqueezeLayer', 'ActNorm1d', 'ActNorm2d', 'LogitTransform',
-           'ZeroMeanTransform', 'squeeze', 'unsqueeze']
+           'ZeroMeanTransform', 'Normalize']
 
 
 def _logp_tensor(logpx, B, device):
@@ -210,3 +210,34 @@ class ZeroMeanTransform(nn.Module):
 
     def inverse(self, y, logpy=None):
         return y + .5 if logpy is None else (y + .5, logpy)
+
+
+class Normalize(nn.Module):
+    """y[:, :c] = (x[:, :c] - mean) / std per channel, log-det -H W sum log|std| (elemwise.py:26-55).
+
+    The init layer train_img.py:230 selects for the classification / hybrid tasks.  Unlike the
+    reference it also accepts the `restore` keyword SequentialFlow passes to every layer."""
+
+    def __init__(self, mean, std):
+        super().__init__()
+        self.register_buffer('mean', torch.as_tensor(mean, dtype=torch.float32))
+        self.register_buffer('std', torch.as_tensor(std, dtype=torch.float32))
+
+    def _per_channel(self, t):
+        return t.view(1, -1, 1, 1)
+
+    def _logdetgrad(self, x):
+        hw = x[0, 0].numel()
+        return (-hw * self.std.abs().log().sum()).expand(x.shape[0], 1)
+
+    def forward(self, x, logpx=None, restore=False):
+        c = self.mean.numel()
+        y = x.clone()
+        y[:, :c] = (x[:, :c] - self._per_channel(self.mean)) / self._per_channel(self.std)
+        return y if logpx is None else (y, logpx - self._logdetgrad(x))
+
+    def inverse(self, y, logpy=None):
+        c = self.mean.numel()
+        x = y.clone()
+        x[:, :c] = y[:, :c] * self._per_channel(self.std) + self._per_channel(self.mean)
+        return x if logpy is None else (x, logpy + self._logdetgrad(x))

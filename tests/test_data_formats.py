@@ -64,7 +64,7 @@ def test_ema_and_checkpoint_roundtrip(tmp_path):
     name, p0 = next(iter(m.named_parameters()))
     np.testing.assert_allclose(ema.shadow_params[name].numpy(), (p0.detach() - 0.5).numpy(), rtol=0, atol=1e-6)
     path = str(tmp_path / 'ck.pth')
-    utils.save_checkpoint(path, m, ema, epoch=3)
+    utils.save_tensor_checkpoint(path, m, ema, epoch=3)
     m2 = build_flow(arch, 4)
     ck, e2 = utils.load_checkpoint(path, m2, use_ema_weights=True)
     assert ck['epoch'] == 3
