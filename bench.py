@@ -89,7 +89,7 @@ MFMA_DESC = {
     'bf16x6': 'bf16x6: fp32 operands split exactly into 3 bf16 pieces, 6 products per fp32 product, fp32 '
               'accumulation (error at fp32 level, tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
     'f16x3': 'f16x3: fp32 operands scaled by 2^s (weights per matrix; activations per pixel column in phases B/C, per '
-             'tile in phase A) and split into 2 fp16 pieces (|x - h - l| <= 2^-24 |x|), 3 products per fp32 product on '
+             'tile in phase A) and split into 2 fp16 pieces (|x - h - l| <= 2^-23 |x|, include/inflow.h), 3 products per fp32 product on '
              'v_mfma_f32_32x32x16_f16, fp32 accumulation, exact unscale (error at fp32 level, '
              'tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
     'f32': 'f32: v_mfma_f32_32x32x2_f32'}

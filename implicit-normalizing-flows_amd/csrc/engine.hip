@@ -114,6 +114,7 @@ struct InfNet {
   int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
+  int fc_block = 1;        // INF_OPT_FC_BLOCK (read on net_z of inf_imblock_eval_exact)
   // fused fc path (fcnet.hip): the whole net in one launch per evaluation (forward and forward-mode Jacobian)
   bool fcfused = false;
   // f16x3 planes of the fused fc layers (fcnet_h3.hip, filled at refresh): layer l at fch + fch_off[l], exponent fchexp[l]
@@ -158,6 +159,12 @@ struct Bufs {
   int nchunk;              // per-sample partial chunks of conv_out (residual norms, unfused series)
   float* Y2;               // fused nets: second taps buffer (series terms alternate Y / Y2)
   int snchunk;             // per-sample partial stride of the series slabs (>= tiles per image)
+  // fc nets: the device-resident block kernel's (fcblock.hip) exchange words and results: [error word, granules]
+  // (zeroed per launch) and [stats, per-sample nstep, lowest_step, prot_break, lowest objective]
+  unsigned* bk_sync;
+  size_t bk_sync_bytes;
+  char* bk_out;
+  size_t bk_out_bytes;
 };
 
 size_t per_sample_hidden(const InfNet* n) { return (size_t)n->hidden_max * (n->fc ? 1 : n->P); }
@@ -200,6 +207,16 @@ size_t carve(const InfNet* n, int B, int T, void* ws, size_t cap, Bufs& b) {
   b.ps_state = w.take<double>((size_t)B * (PS_HEAD + T));
   b.ps_active = w.take<int>((size_t)B);
   b.ps_improved = w.take<int>((size_t)B);
+  if (n->fc) {
+    b.bk_sync_bytes = 16 + sizeof(unsigned long long) * 8 * (size_t)fcblock_grid(B);   // 4 sets x 2 granules
+    b.bk_sync = reinterpret_cast<unsigned*>(w.take<char>(b.bk_sync_bytes));
+    b.bk_out_bytes = sizeof(FcBlockStats) + (sizeof(int) * 3 + sizeof(double)) * (size_t)B + 64;
+    b.bk_out = w.take<char>(b.bk_out_bytes);
+  } else {
+    b.bk_sync = nullptr;
+    b.bk_out = nullptr;
+    b.bk_sync_bytes = b.bk_out_bytes = 0;
+  }
   return w.off + 256;
 }
 
@@ -828,7 +845,12 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
         }
         if (!allow) break;                                              // nstep == T
       }
-      if (!spec) INF_TRY(enqueue_next(nstep));
+      if (!spec) {
+        // the loop goes on past the iterate the tail was queued for: that iterate is no longer the candidate result,
+        // and its buffers go back to the pools (a later iterate may reuse them), so the tail no longer names it
+        if (tail) tail->x = tail->f = nullptr;
+        INF_TRY(enqueue_next(nstep));
+      }
       xp = xs;
       fp = fs;
       ps_ = 1 - ps_;
@@ -1022,6 +1044,128 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     stats.fixed_point_iters = it;
   }
   if (st) *st = stats;
+  return INF_OK;
+}
+
+// inf_imblock_eval_exact on the device-resident block kernel (fcblock.hip): one launch, one readback of its
+// statistics; a protective break runs the Banach fallback and the recompute on the host path (as below).
+static thread_local char* g_bk_host = nullptr;
+static thread_local size_t g_bk_host_cap = 0;
+int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B, int T,
+                  double eps_in, InfBroydenStats* stats, Bufs& bf, hipStream_t s) {
+  if (nx->mfma_mode != INF_MFMA_F16X3 || nz->mfma_mode != INF_MFMA_F16X3 || !bf.bk_sync) return INF_ERR_UNSUPPORTED;
+  FcBlockArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nx = fc_args(nx, nullptr, B);
+  a.nz = fc_args(nz, nullptr, B);
+  a.B = B;
+  a.T = T;
+  a.per_sample = nz->convergence == INF_CONV_PER_SAMPLE;
+  if (!fcblock_supported(a)) return INF_ERR_UNSUPPORTED;
+  const int d = nz->d;
+  a.eps = eps_in * sqrt((double)B * d);                              // broyden.py:131
+  a.eps_ps = eps_in * sqrt((double)d);
+  a.x = x;
+  a.z = z;
+  a.logdet_x = logdet_x;
+  a.logdet_z = logdet_z;
+  a.xin_g = bf.xin;
+  a.fx_g = bf.fx;
+  a.xemb_g = bf.xemb;
+  a.lowx_g = bf.lowest;
+  a.lowf_g = bf.flow;
+  a.error = bf.bk_sync;
+  a.gran = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(bf.bk_sync) + 16);
+  a.tag0 = 1;
+  FcBlockStats* dst = reinterpret_cast<FcBlockStats*>(bf.bk_out);
+  a.stats = dst;
+  a.s_nstep = reinterpret_cast<int*>(bf.bk_out + sizeof(FcBlockStats));
+  a.s_lstep = a.s_nstep + B;
+  a.s_prot = a.s_lstep + B;
+  a.s_lowest = reinterpret_cast<double*>(bf.bk_out + ((sizeof(FcBlockStats) + sizeof(int) * 3 * (size_t)B + 7) & ~(size_t)7));
+  INF_HIP(hipMemsetAsync(bf.bk_sync, 0, bf.bk_sync_bytes, s));
+  {
+    const int st = launch_fcblock(a, s);
+    if (st != INF_OK) return st;
+  }
+  // one readback: the error word and the statistics (per-sample rule: the per-sample arrays too)
+  const size_t nbytes = a.per_sample ? bf.bk_out_bytes : sizeof(FcBlockStats);
+  if (g_bk_host_cap < nbytes + 16) {
+    if (g_bk_host) (void)hipHostFree(g_bk_host);
+    g_bk_host = nullptr;
+    g_bk_host_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&g_bk_host), nbytes + 16, hipHostMallocDefault) != hipSuccess)
+      return INF_ERR_HIP;
+    g_bk_host_cap = nbytes + 16;
+  }
+  INF_HIP(hipMemcpyAsync(g_bk_host, bf.bk_sync, 16, hipMemcpyDeviceToHost, s));
+  INF_HIP(hipMemcpyAsync(g_bk_host + 16, bf.bk_out, nbytes, hipMemcpyDeviceToHost, s));
+  hipEvent_t ev = nullptr;
+  {
+    static thread_local hipEvent_t bk_ev = nullptr;
+    if (!bk_ev && hipEventCreateWithFlags(&bk_ev, hipEventDisableTiming) != hipSuccess) return INF_ERR_HIP;
+    ev = bk_ev;
+  }
+  INF_HIP(hipEventRecord(ev, s));
+  INF_TRY(host_wait(ev));
+  if (*reinterpret_cast<unsigned*>(g_bk_host) != 0) {
+    set_hip_error(hipErrorLaunchTimeOut);
+    return INF_ERR_HIP;
+  }
+  const FcBlockStats* hs = reinterpret_cast<const FcBlockStats*>(g_bk_host + 16);
+  InfBroydenStats st = stats_for(stats);
+  st.convergence = nz->convergence;
+  if (!a.per_sample) {
+    st.nstep = hs->nstep;
+    st.lowest_step = hs->lowest_step;
+    st.prot_break = hs->prot_break;
+    st.n_trace = std::min(hs->n_trace, 64);
+    for (int k = 0; k < st.n_trace; ++k) st.trace[k] = hs->trace[k];
+    st.diff = hs->lowest;
+    st.eps = a.eps;
+  } else {
+    const char* base = g_bk_host + 16;
+    const int* sn = reinterpret_cast<const int*>(base + sizeof(FcBlockStats));
+    const int* sl = sn + B;
+    const int* sp = sl + B;
+    const double* slo = reinterpret_cast<const double*>(
+        base + ((sizeof(FcBlockStats) + sizeof(int) * 3 * (size_t)B + 7) & ~(size_t)7));
+    double d2 = 0.0;
+    for (int b = 0; b < B; ++b) {
+      st.nstep = std::max(st.nstep, sn[b]);
+      st.lowest_step = std::max(st.lowest_step, sl[b]);
+      st.prot_break |= sp[b];
+      d2 += slo[b] * slo[b];
+      if (st.sample_nstep) st.sample_nstep[b] = sn[b];
+      if (st.sample_lowest_step) st.sample_lowest_step[b] = sl[b];
+      if (st.sample_prot_break) st.sample_prot_break[b] = sp[b];
+    }
+    st.diff = sqrt(d2);
+    st.eps = a.eps_ps;
+  }
+  if (st.prot_break) {
+    // banach_find_root (implicit_block.py:57-65,74-75) from z0 = x, as broyden_solve does, on the buffers the kernel
+    // left: x_embed, f_x(x), x and the lowest iterates (per-sample rule: only the samples whose own solve broke)
+    std::vector<int> todo;
+    if (a.per_sample) {
+      const int* sp = reinterpret_cast<const int*>(g_bk_host + 16 + sizeof(FcBlockStats)) + 2 * B;
+      todo.assign(sp, sp + B);
+    }
+    int it = 0;
+    INF_TRY(banach_solve(nz, bf.xin, B, eps_in, 1000, todo.empty() ? nullptr : todo.data(), bf, s, &it));
+    st.fixed_point_iters = it;
+    OutArgs o;
+    memset(&o, 0, sizeof(o));
+    o.in0 = bf.fx;
+    o.in1 = bf.xin;
+    o.out0 = bf.tmp;
+    INF_TRY(run_forward(nz, bf.lowest, B, bf, OM_RECOMP, &o, s));
+    FcArgs fjz = fc_args(nz, bf.tmp, B);
+    fjz.logdet = logdet_z;
+    INF_TRY(launch_fcnet(fjz, true, s));
+    INF_TRY(to_boundary(nx, bf.tmp, z, B, s));
+  }
+  if (stats) *stats = st;
   return INF_OK;
 }
 
@@ -1412,7 +1556,8 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     static const char* const conv_v[] = {"global", "per_sample"};
     const EnvOpt opts[] = {{"INFLOW_FUSED_K128", &n->k128, k128_v, 3},
                            {"INFLOW_EVAL_OVERLAP", &n->eval_overlap, bin_v, 2},
-                           {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2}};
+                           {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2},
+                           {"INFLOW_FC_BLOCK", &n->fc_block, k128_v, 3}};
     for (const EnvOpt& o : opts) {
       const char* e = getenv(o.name);
       if (!e || !*e) continue;
@@ -1478,6 +1623,8 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
 
 int inf_net_set_mfma(InfNet* n, int mode) {
   if (!n || (mode != INF_MFMA_F32 && mode != INF_MFMA_BF16X6 && mode != INF_MFMA_F16X3)) return INF_ERR_INVALID;
+  // the cached f(0) (ensure_f0) carries the bits of the arithmetic it was computed with
+  if (n->mfma_mode != mode) n->f0_batch = -1;
   n->mfma_mode = mode;
   return INF_OK;
 }
@@ -1904,6 +2051,13 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
   // x in the internal layout: written by the x-branch JAC launch's staging (it reads x in the boundary layout)
   const float* xi = bf.xin;
+  if (nz->fc_block == 2 || (nz->fc_block == 1 && nz->convergence == INF_CONV_PER_SAMPLE)) {
+    // the whole block in one launch (fcblock.hip); falls through to the launch-per-iteration path below when the
+    // configuration has no block kernel or (global rule) its grid cannot be co-resident.  The default (1) takes it for
+    // the per-sample rule only: under the global rule the launch path is faster
+    const int st = fc_block_eval(nx, nz, x, z, logdet_x, logdet_z, B, T, eps, stats, bf, s);
+    if (st != INF_ERR_UNSUPPORTED) return st;
+  }
   // log|det(I + J_fx(x))| (implicit_block.py:358-362) and x_embed = f_x(x) + x (:71) in one launch: the JAC kernel's primal
   // column is f_x(x) with the FWD kernel's bits (the same 16-column tiles, k slices and partial order), so the x_embed
   // launch is folded into it.  (Run beside the root solve on the side stream instead, the JAC launch took every CU
@@ -1951,6 +2105,65 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   fjz.logdet = logdet_z;
   INF_TRY(launch_fcnet(fjz, true, s));
   return to_boundary(nx, bf.tmp, z, B, s);
+}
+
+size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int batch, const int* thresholds) {
+  if (!net_z || n_blocks <= 0 || batch <= 0 || !thresholds) return 0;
+  size_t blk = 0;
+  for (int i = 0; i < n_blocks; ++i)
+    if (net_z[i]) blk = std::max(blk, inf_workspace_bytes(net_z[i], batch, thresholds[i]));
+  const size_t d = net_z[0] ? (size_t)net_z[0]->d : 0;
+  return blk + 256 * 4 + sizeof(float) * ((size_t)2 * batch * d + (size_t)4 * batch);
+}
+
+// SequentialFlow of fc imBlocks in eval (train_tabular.py:314-336; container.py:12-20): block i is
+// inf_imblock_eval_exact on the previous block's z, its log-density step logp <- logp - (logdet_x - logdet_z) on the device
+// (implicit_block.py:234), the blocks back to back on the stream with no host round trip between them beyond the ones a
+// block itself makes.
+int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_blocks, const float* x, float* z,
+                              const float* logp_in, float* logp_out, int B, const int* thresholds, const double* eps,
+                              InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
+  if (!net_x || !net_z || n_blocks <= 0 || !x || !z || !logp_out || B <= 0 || !thresholds || !eps || x == z)
+    return INF_ERR_INVALID;
+  for (int i = 0; i < n_blocks; ++i) {
+    InfNet *nx = net_x[i], *nz = net_z[i];
+    if (!nx || !nz || !same_shape(nx, nz) || !same_shape(nz, net_z[0]) || thresholds[i] <= 0 || thresholds[i] > 64)
+      return INF_ERR_INVALID;
+    if (!nx->fcfused || !nz->fcfused || nx->d > 10) return INF_ERR_UNSUPPORTED;
+    FcArgs px = fc_args(nx, x, B), pz = fc_args(nz, x, B);
+    if (!fcnet_supported(px, true) || !fcnet_supported(pz, true)) return INF_ERR_UNSUPPORTED;
+  }
+  if (!ws || ws_bytes < inf_flow_chain_workspace_bytes(net_z, n_blocks, B, thresholds)) return INF_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t E = (size_t)B * net_z[0]->d;
+  char* base = reinterpret_cast<char*>(ws);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    char* p = base + off;
+    off += bytes;
+    return reinterpret_cast<float*>(p);
+  };
+  float* zb[2] = {take(sizeof(float) * E), take(sizeof(float) * E)};
+  float* ldx = take(sizeof(float) * B);
+  float* ldz = take(sizeof(float) * B);
+  float* lp[2] = {take(sizeof(float) * B), take(sizeof(float) * B)};
+  off = (off + 255) & ~(size_t)255;
+  void* bws = base + off;
+  const size_t bws_bytes = ws_bytes - off;
+  const float* in = x;
+  const float* lin = logp_in;
+  for (int i = 0; i < n_blocks; ++i) {
+    const bool last = i == n_blocks - 1;
+    float* out = last ? z : zb[i & 1];
+    float* lout = last ? logp_out : lp[i & 1];
+    INF_TRY(inf_imblock_eval_exact(net_x[i], net_z[i], in, out, ldx, ldz, B, thresholds[i], eps[i],
+                                   stats ? &stats[i] : nullptr, bws, bws_bytes, stream));
+    INF_TRY(glue_logp_step(lin, ldx, ldz, lout, B, s));
+    in = out;
+    lin = lout;
+  }
+  return INF_OK;
 }
 
 int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
@@ -2408,6 +2621,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
     case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;
+    case INF_OPT_FC_BLOCK: slot = &n->fc_block; hi = 2; break;
     default: return -INF_ERR_INVALID;
   }
   if (value < lo || value > hi) return -INF_ERR_INVALID;
@@ -2425,6 +2639,7 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_EVAL_OVERLAP: return n->eval_overlap;
     case INF_OPT_CONVERGENCE: return n->convergence;
     case INF_OPT_K128_EXACT_SCALE: return n->exact_scale;
+    case INF_OPT_FC_BLOCK: return n->fc_block;
     default: return -INF_ERR_INVALID;
   }
 }

@@ -12,6 +12,7 @@ int glue_poison_lds(hipStream_t s);
 int glue_add(const float* a, const float* b, float* out, long n, hipStream_t s);
 size_t glue_batched_dot_scratch(int B, long per);
 int glue_batched_dot(const float* a, const float* c, float* out, int B, long per, double* scratch, hipStream_t s);
+int glue_logp_step(const float* lin, const float* ldx, const float* ldz, float* lout, int B, hipStream_t s);
 int glue_recomp(const float* fx, const float* fz, const float* x, float* out, long n, hipStream_t s);
 int glue_fixed_point_check(const float* x, const float* xp, const float* y, long n, float eps, unsigned int* count,
                            hipStream_t s);

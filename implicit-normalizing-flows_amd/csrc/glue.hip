@@ -191,6 +191,17 @@ int glue_add(const float* a, const float* b, float* out, long n, hipStream_t s) 
   return INF_OK;
 }
 
+__global__ void logp_step_kernel(const float* lin, const float* ldx, const float* ldz, float* lout, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) lout[b] = (lin ? lin[b] : 0.f) - (ldx[b] - ldz[b]);
+}
+// one imBlock's log-density step (implicit_block.py:234: logpx - logdet, logdet = logdet_x - logdet_z); lin null: 0
+int glue_logp_step(const float* lin, const float* ldx, const float* ldz, float* lout, int B, hipStream_t s) {
+  hipLaunchKernelGGL(logp_step_kernel, dim3((B + 255) / 256), dim3(256), 0, s, lin, ldx, ldz, lout, B);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 __global__ void recomp_kernel(const float* fx, const float* fz, const float* x, float* out, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (fx[i] - fz[i]) + x[i];

@@ -257,6 +257,38 @@ int launch_fc_split_h3(const float* A, int M, int Kpad, int nrt, int nks, uint16
 // *exp_out = h3_scale_exp(max |src|) (pointwise.hip)
 int launch_amax_exp(const float* src, long n, int* exp_out, hipStream_t s);
 
+// one launch per fused fc imBlock evaluation (fcblock.hip): x-branch log-det and x_embed, the Broyden root solve with its
+// state in LDS (global rule: one tagged fp64 partial per workgroup and iteration; per-sample rule: no exchange), the z
+// recompute and the z-branch log-det
+struct FcBlockStats {     // global rule (written by workgroup 0)
+  int nstep, lowest_step, prot_break, n_trace;
+  double lowest;
+  double trace[64];
+};
+struct FcBlockArgs {
+  FcArgs nx, nz;          // the two nets (f16x3 planes); their x / o / br fields are unused
+  int B, T, per_sample;
+  double eps, eps_ps;     // eps sqrt(B d) (global rule), eps sqrt(d) (per sample)
+  const float* x;         // (B, d) boundary layout
+  float* z;               // (B, d)
+  float* logdet_x;        // (B)
+  float* logdet_z;        // (B)
+  // internal (d, B) copies for the host's Banach fallback: x, f_x(x), x_embed, the lowest iterate and its f
+  float *xin_g, *fx_g, *xemb_g, *lowx_g, *lowf_g;
+  unsigned long long* gran;   // 4 sets x grid x 2 granules, zeroed before the launch (with the error word and counter)
+  unsigned tag0;              // tag of iteration 0 (> 0); iteration k uses tag0 + k
+  FcBlockStats* stats;
+  int *s_nstep, *s_lstep, *s_prot;   // per-sample rule: per sample (B)
+  double* s_lowest;
+  unsigned* error;            // [0] set when a spin timed out, [1] the exchange's arrival counter
+  unsigned long long* tbuf;   // phase stamps (INFLOW_PHASE_STAMPS builds), else null
+};
+int fcblock_supported(const FcBlockArgs& a);
+int fcblock_grid(int B);
+size_t fcblock_lds_bytes(int d, int T);
+// INF_ERR_UNSUPPORTED when the configuration has no kernel or (global rule) the grid cannot be co-resident
+int launch_fcblock(const FcBlockArgs& a, hipStream_t s);
+
 // ------------------------------------------------------------------------------------------
 // parameter gradients (grad.hip)
 // ------------------------------------------------------------------------------------------

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
 INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE, INF_OPT_K128_EXACT_SCALE = 1, 2, 3, 4   # InfNetOption
+INF_OPT_FC_BLOCK = 5
 INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
 CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 
@@ -102,6 +103,12 @@ _SIGS = {
                                         ctypes.c_size_t, _P]),
     'inf_imblock_eval_exact': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                               ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
+    'inf_flow_chain_workspace_bytes': (ctypes.c_size_t, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int,
+                                                         ctypes.POINTER(ctypes.c_int)]),
+    'inf_flow_eval_exact_chain': (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.c_int, _P, _P, _P, _P,
+                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(BroydenStats), _P,
+                                                 ctypes.c_size_t, _P]),
     'inf_imblock_backward': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                             ctypes.POINTER(BroydenStats), _P, ctypes.c_size_t, _P]),
     'inf_imblock_forward': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,

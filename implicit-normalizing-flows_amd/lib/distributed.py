@@ -48,20 +48,14 @@ class PendingPair:
     behind it; get() waits for that copy only.  An evaluation loop that calls get() for batch i after enqueueing batch
     i + 1 never lets the GPU drain between batches (the host's Python for the next batch overlaps this batch's tail)."""
 
-    _ring = {}
-
     def __init__(self, t):
         dev = t.device
         if dev.type != 'cuda':
             self.host, self.ev = t, None
             return
-        ring = PendingPair._ring.get(dev.index)
-        if ring is None:
-            ring = PendingPair._ring[dev.index] = [[torch.empty(2, dtype=torch.float64, pin_memory=True), 0]
-                                                   for _ in range(4)]
-        slot = min(ring, key=lambda r: r[1])          # the least recently used of 4 pinned buffers
-        slot[1] = max(r[1] for r in ring) + 1
-        self.host = slot[0]
+        # a pinned buffer of its own: torch's caching host allocator hands a block out again only after the copy
+        # recorded on it has completed, so any number of pairs can be pending at once
+        self.host = torch.empty(2, dtype=torch.float64, pin_memory=True)
         self.host.copy_(t, non_blocking=True)
         self.ev = torch.cuda.Event()
         self.ev.record(torch.cuda.current_stream(dev))

@@ -33,6 +33,12 @@ class SequentialFlow(nn.Module):
         self.chain = nn.ModuleList(layersList)
 
     def forward(self, x, logpx=None, restore=False):
+        if logpx is not None and not restore and not self.training and x.is_cuda:
+            # a chain of fc imBlocks in eval (the tabular / toy models): one engine call for all blocks
+            from .imblock import eval_exact_chain
+            out = eval_exact_chain(list(self.chain), x, logpx)
+            if out is not None:
+                return out
         if logpx is None:
             for layer in self.chain:
                 x = layer(x, restore=restore)

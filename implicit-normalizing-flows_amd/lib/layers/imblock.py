@@ -257,6 +257,51 @@ def _uninitialised_convs(net):
     return any(getattr(m, 'initialized', 1) == 0 for m in net.modules() if hasattr(m, 'spatial_dims'))
 
 
+def eval_exact_chain(blocks, x, logpx):
+    """A SequentialFlow of fc imBlocks in eval (train_tabular.py:314-336) in one engine call
+    (inf_flow_eval_exact_chain): every block's inf_imblock_eval_exact back to back on the stream, the log-density
+    steps on the device.  Returns (z, logpx (B, 1)), or None when a block is not eligible (the caller then runs the
+    blocks one by one; nothing has run)."""
+    if (x.dim() != 2 or x.shape[1] > 10 or not x.is_cuda or x.dtype != torch.float32 or not blocks or
+            any(not isinstance(b, imBlock) or b.training or b.exact_trace or _needs_graph(b, x) for b in blocks)):
+        return None
+    from .flows import _logp_tensor
+    lib = _hip.load()
+    x = x.contiguous()
+    B, n = x.shape[0], len(blocks)
+    natives = [b._native(x) for b in blocks]
+    stream = natives[0][2]
+    nx = (ctypes.c_void_p * n)(*[p[0].handle.value for p in natives])
+    nz = (ctypes.c_void_p * n)(*[p[1].handle.value for p in natives])
+    T = (ctypes.c_int * n)(*[int(b.threshold) for b in blocks])
+    eps = (ctypes.c_double * n)(*[float(b.eps_forward) for b in blocks])
+    stats = (_hip.BroydenStats * n)()
+    samples = []
+    for i, p in enumerate(natives):
+        if p[1].get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE:
+            arrs = [(ctypes.c_int * B)() for _ in range(3)]
+            stats[i].sample_nstep, stats[i].sample_lowest_step, stats[i].sample_prot_break = [
+                ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in arrs]
+            samples.append(arrs)
+        else:
+            samples.append(None)
+    ws = _hip.workspace(x.device, lib.inf_flow_chain_workspace_bytes(nz, n, B, T))
+    z = torch.empty_like(x)
+    lp_in = _logp_tensor(logpx, B, x.device)
+    lp_out = torch.empty(B, device=x.device)
+    rc = lib.inf_flow_eval_exact_chain(nx, nz, n, _hip.ptr(x), _hip.ptr(z), _hip.ptr(lp_in) if lp_in is not None else None,
+                                       _hip.ptr(lp_out), B, T, eps, stats, _hip.ptr(ws), ws.numel(), stream)
+    if rc == _hip.INF_ERR_UNSUPPORTED:
+        return None
+    _hip.check(rc, 'inf_flow_eval_exact_chain')
+    for i, b in enumerate(blocks):
+        d = stats[i].as_dict(int(b.threshold))
+        if samples[i] is not None:
+            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in samples[i]]
+        b.last_broyden = d
+    return z, lp_out.view(B, 1)
+
+
 class imBlock(nn.Module):
 
     def __init__(self, nnet_x, nnet_z, geom_p=0.5, lamb=2., n_power_series=None, exact_trace=False,

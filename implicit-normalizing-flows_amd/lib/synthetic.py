@@ -340,6 +340,57 @@ def prot_break_batch(seed=5):
     return x
 
 
+# A deep variant with the POWER nets' shape (6-128-128-128-128-6, Sin), so the fused fc paths and the device-resident
+# block kernel (fcblock.hip) take it: nnet_x == 0; nnet_z has one coupling path z0 -> unit 0 of every hidden layer ->
+# f1 with gain G per layer and C at the output, every matrix holding a single magnitude (which the scaled fp16 split
+# represents to 2^-23 relative).  With x ~ 1e-9, Broyden's first step z = -x gives f1 ~ C s(G^4 x0) ~ 0.6 x0 / 1e-9
+# against |g(0)| ~ 1e-9: the residual grows by ~1e8 (prot_break).  f1 depends on z0 only, which the Banach iteration
+# fixes at x0 on its first pass, so it stops with an exactly-zero change on the next; the samples with x0 == 0
+# converge in Broyden (per-sample rule).  J_f is nilpotent: the exact log-dets are 0 up to rounding.
+PROT_BREAK_DEEP = dict(d=6, hidden=128, n_hidden=3, G=100.0, C=6.0, coeff=1e12, eps_forward=1e-13, x_scale=1e-9,
+                       zero_rows=(1, 4), B=6)
+
+
+def prot_break_deep_nets_state():
+    """State dict of the deep prot_break imBlock (Sequential of InducedNormLinear / Sin, keys 0, 2, 4, 6, 8, and the
+    frozen copies); u / v are the exact top singular vectors (sigma = G, G, G, G, C, far below coeff: W_eff == W)."""
+    p = PROT_BREAK_DEEP
+    d, h, nh = p['d'], p['hidden'], p['n_hidden']
+    shapes = [(h, d)] + [(h, h)] * nh + [(d, h)]
+    e = lambda n, i: _t(np.eye(n, dtype=np.float32)[i])
+    sd = OrderedDict()
+    sd['lamb'] = torch.tensor(2.0)
+    sd['last_n_samples'] = torch.zeros(1)
+    sd['last_firmom'] = torch.zeros(1)
+    sd['last_secmom'] = torch.zeros(1)
+    for net in ('nnet_x', 'nnet_z'):
+        zero = net == 'nnet_x'
+        for l, (o, i) in enumerate(shapes):
+            W = np.zeros((o, i), np.float32)
+            last = l == len(shapes) - 1
+            gain = p['C'] if last else p['G']
+            if not zero:
+                W[1 if last else 0, 0] = gain
+            k = '%s.%d.' % (net, 2 * l)
+            sd[k + 'weight'] = _t(W)
+            sd[k + 'bias'] = torch.zeros(o)
+            sd[k + 'scale'] = torch.tensor(0. if zero else float(gain))
+            sd[k + 'u'], sd[k + 'v'] = e(o, 1 if last else 0), e(i, 0)
+    for k in list(sd.keys()):
+        if k.startswith('nnet_'):
+            sd[k.replace('nnet_x.', 'nnet_x_copy.', 1).replace('nnet_z.', 'nnet_z_copy.', 1)] = sd[k].clone()
+    return sd
+
+
+def prot_break_deep_batch(seed=6):
+    p = PROT_BREAK_DEEP
+    g = torch.Generator().manual_seed(int(seed))
+    x = torch.randn(p['B'], p['d'], generator=g) * p['x_scale']
+    for r in p['zero_rows']:
+        x[r, 0] = 0.
+    return x
+
+
 def perturbed_weight(sd, key, seed=1, scale=0.05):
     """sd[key + '.weight'] moved off its converged u / v (as after an optimiser step): W + scale * std(W) * N(0, 1),
     deterministic (numpy PCG64 keyed like the weights).  Power-iteration fixtures start from it."""

@@ -135,13 +135,21 @@ int inf_net_get_mfma(const InfNet* net);
  *   INF_OPT_K128_EXACT_SCALE  0 (default) / 1: the 128-pixel kernel puts chunk 1's phase-A values at chunk 0's column
  *                         scales and falls back to exact per-chunk scales only for a tile where a value would not fit
  *                         fp16; 1 takes the exact-scale path on every tile (tests: both paths give the same results).
- * Unknown values of INFLOW_FUSED_K128 (0/1/2), INFLOW_EVAL_OVERLAP (0/1) and INFLOW_CONVERGENCE (global/per_sample)
+ *   INF_OPT_FC_BLOCK      read on net_z of inf_imblock_eval_exact: where a block kernel exists (fcblock.hip: f16x3
+ *                         nets, d = 6 with 3 hidden layers or d = 2 with 1, threshold <= 30; the global rule also needs
+ *                         the grid co-resident: batch <= 48 x the co-resident workgroups) the whole block runs in one
+ *                         launch, the Broyden state in LDS, the global rule's norm exchanged between workgroups inside
+ *                         the launch, the host reading the statistics once.  0 never; 1 (default; INFLOW_FC_BLOCK at
+ *                         create) for the per-sample rule only, where it is the faster path; 2 for both rules.
+ *                         Otherwise every net evaluation is a launch and the host reads each iteration's norm.
+ * Unknown values of INFLOW_FUSED_K128 / INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP (0/1) and INFLOW_CONVERGENCE (global/per_sample)
  * make inf_net_create fail with INF_ERR_INVALID.
  * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
  * runs the VJP as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322); results
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
-  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4
+  INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4,
+  INF_OPT_FC_BLOCK = 5
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);
@@ -213,6 +221,16 @@ int inf_imblock_eval(InfNet* net_x, InfNet* net_z, const float* x, float* z, con
 int inf_imblock_eval_exact(InfNet* net_x, InfNet* net_z, const float* x, float* z, float* logdet_x, float* logdet_z,
                            int batch, int threshold, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes,
                            void* stream);
+/* A SequentialFlow of such fc imBlocks in eval (train_tabular.py:314-336, container.py:12-20) in one call: block i runs
+ * inf_imblock_eval_exact on block i-1's z (block 0 on x) and the log-density step logp <- logp - (logdet_x - logdet_z)
+ * on the device (implicit_block.py:234; logp_in NULL: 0), writing the last block's z and the final logp (batch).  No
+ * host round trip between blocks beyond a block's own.  thresholds / eps: per block; stats: n_blocks entries or NULL.
+ * INF_ERR_UNSUPPORTED (before any launch) when a block is not on the fused fc path.
+ * ws >= inf_flow_chain_workspace_bytes(net_z, n_blocks, batch, thresholds). */
+size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int batch, const int* thresholds);
+int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_blocks, const float* x, float* z,
+                              const float* logp_in, float* logp_out, int batch, const int* thresholds,
+                              const double* eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream);
 /* Neumann gradient surrogate value (implicit_block.py:429-438): w = sum_{k=0}^{n} ncoeff[k] (J^T)^k eps,
  * out[b] = <J^T w, eps>.  ncoeff is a HOST array of n_terms+1 values ((-1)^k c_k, ncoeff[0] = 1). */
 int inf_logdet_neumann(InfNet* net, const float* x, const float* vareps, const float* ncoeff, int n_terms,

@@ -17,6 +17,8 @@ container only; same harness as make_golden.py: its import shims, model builders
   stall_small_b4       iterate) and at the stall break (broyden.py:165-168: threshold 1, eps = obj_1 / 2)
   degenerate_small_b4  v^T dg == 0 for one sample (identical nets, a zero sample: g(0) == 0 exactly), the NaN
                        scrub of broyden.py:177-178
+  prot_break_b6        Broyden's protective break and the Banach fallback (fc imBlock, lib/synthetic.py PROT_BREAK)
+  prot_break_deep_b6   the same on the POWER nets' shape (PROT_BREAK_DEEP: the fused fc and block-kernel paths)
   cifar_small_b4_ps    per-sample convergence: the reference's broyden run on each sample as a batch of one
   cifar_full_b8_ps     (the root solves; probes and series lengths as in the batched run)
 """
@@ -338,24 +340,34 @@ def per_sample_broyden(orig):
 
 
 # ---- a3: protective break -> Banach fallback ------------------------------------------------------------
-def _prot_break_block():
-    p = syn.PROT_BREAK
+def _prot_break_block(deep=False):
+    p = syn.PROT_BREAK_DEEP if deep else syn.PROT_BREAK
     lin = lambda a, b: base_layers.InducedNormLinear(a, b, coeff=p['coeff'], n_iterations=None, atol=1e-3, rtol=1e-3,
                                                      domain=2, codomain=2)
-    net = lambda: torch.nn.Sequential(lin(p['d'], p['hidden']), base_layers.Sin(), lin(p['hidden'], p['d']))
+
+    def net():
+        if not deep:
+            return torch.nn.Sequential(lin(p['d'], p['hidden']), base_layers.Sin(), lin(p['hidden'], p['d']))
+        mods = [lin(p['d'], p['hidden'])]
+        for _ in range(p['n_hidden']):
+            mods += [base_layers.Sin(), lin(p['hidden'], p['hidden'])]
+        return torch.nn.Sequential(*mods, base_layers.Sin(), lin(p['hidden'], p['d']))
     blk = layers.imBlock(net(), net(), n_dist='geometric', n_power_series=None, exact_trace=False, brute_force=False,
                          n_samples=1, n_exact_terms=2, neumann_grad=False, grad_in_forward=False,
                          eps_forward=p['eps_forward'])
-    blk.load_state_dict(syn.prot_break_nets_state(), strict=True)
+    blk.load_state_dict(syn.prot_break_deep_nets_state() if deep else syn.prot_break_nets_state(), strict=True)
     return blk.eval()
 
 
-def prot_break_case(seed=5):
+def prot_break_case(seed=5, deep=False):
     """One fc imBlock (lib/synthetic.py PROT_BREAK) whose Broyden solve breaks at its first step: the batch
     (broyden.py:169-172 -> implicit_block.py:74-75, find_fixed_point from z0 = x with eps_forward and 1000
     iterations), and each sample as a batch of one (broyden_find_root per sample: only the samples whose own solve
     breaks take the fixed point)."""
-    x = syn.prot_break_batch(seed)
+    x = syn.prot_break_deep_batch(seed) if deep else syn.prot_break_batch(seed)
+    if deep:   # every coupled sample breaks by a wide margin: G^4 |x0| >= 5e-3 (f1 / |g(0)| >~ 1e7)
+        x0 = x[:, 0].abs() / syn.PROT_BREAK_DEEP['x_scale']
+        assert all(float(v) > 0.05 for i, v in enumerate(x0) if i not in syn.PROT_BREAK_DEEP['zero_rows']), x0
     B = x.shape[0]
     counts = {'g': 0, 'fp': []}
     orig_ffp = ib.find_fixed_point
@@ -373,7 +385,7 @@ def prot_break_case(seed=5):
     orig_bfr = ib.RootFind.broyden_find_root
     try:
         for tag, per_sample in (('g', False), ('ps', True)):
-            blk = _prot_break_block()
+            blk = _prot_break_block(deep)
             counts['fp'] = []
             stats = []
 
@@ -421,11 +433,12 @@ def prot_break_case(seed=5):
                 print('      trace', np.array2string(s['trace'], precision=3))
     finally:
         ib.find_fixed_point = orig_ffp
-    _save('prot_break_b6', out)
+    _save('prot_break_deep_b6' if deep else 'prot_break_b6', out)
 
 
 CASES = {
     'prot_break_b6': prot_break_case,
+    'prot_break_deep_b6': lambda: prot_break_case(seed=6, deep=True),
     'power_iter_layers': power_iter_layers,
     'inverse_small_b4': lambda: inverse_case('inverse_small_b4', syn.CIFAR10_SMALL, 4, 12),
     'inverse_full_b2': lambda: inverse_case('inverse_full_b2', syn.CIFAR10, 2, 13),
