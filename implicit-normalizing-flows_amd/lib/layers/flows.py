@@ -36,7 +36,7 @@ class SequentialFlow(nn.Module):
         if logpx is not None and not restore and not self.training and x.is_cuda:
             # a chain of fc imBlocks in eval (the tabular / toy models): one engine call for all blocks
             from .imblock import eval_exact_chain
-            out = eval_exact_chain(list(self.chain), x, logpx)
+            out = eval_exact_chain(list(self.chain), x, logpx, owner=self)
             if out is not None:
                 return out
         if logpx is None:

@@ -257,11 +257,56 @@ def _uninitialised_convs(net):
     return any(getattr(m, 'initialized', 1) == 0 for m in net.modules() if hasattr(m, 'spatial_dims'))
 
 
-def eval_exact_chain(blocks, x, logpx):
+class _ChainPlan:
+    """The host-side state of inf_flow_eval_exact_chain for one (model, batch shape, device, convergence settings):
+    the native nets of every block, the ctypes argument arrays, the statistics buffers and the workspace.  Reused while
+    the engine tensors of every net keep their storage and version (a weight update re-runs the blocks' refresh)."""
+
+    def __init__(self, blocks, x):
+        lib = _hip.load()
+        B, n = x.shape[0], len(blocks)
+        self.B = B
+        self.natives = [b._native(x) for b in blocks]
+        self.stream = self.natives[0][2]
+        self.nx = (ctypes.c_void_p * n)(*[p[0].handle.value for p in self.natives])
+        self.nz = (ctypes.c_void_p * n)(*[p[1].handle.value for p in self.natives])
+        self.T = (ctypes.c_int * n)(*[int(b.threshold) for b in blocks])
+        self.eps = (ctypes.c_double * n)(*[float(b.eps_forward) for b in blocks])
+        self.stats = (_hip.BroydenStats * n)()
+        self.samples = []
+        for i, p in enumerate(self.natives):
+            if p[1].get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE:
+                arrs = [(ctypes.c_int * B)() for _ in range(3)]
+                self.stats[i].sample_nstep, self.stats[i].sample_lowest_step, self.stats[i].sample_prot_break = [
+                    ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in arrs]
+                self.samples.append(arrs)
+            else:
+                self.samples.append(None)
+        self.ws = _hip.workspace(x.device, lib.inf_flow_chain_workspace_bytes(self.nz, n, B, self.T))
+        self.tensors = [t for p in self.natives for nn_ in p[:2] for t in nn_._tensors]
+        self.sig = self.signature()
+
+    def signature(self):
+        return [(t.data_ptr(), t._version) for t in self.tensors]
+
+
+def _chain_eligible(native_z):
+    """Whether the blocks run as block-kernel launches (INF_OPT_FC_BLOCK on the solved net), where the chain call pays."""
+    fcb = native_z.get_option(_hip.INF_OPT_FC_BLOCK)
+    return fcb == 2 or (fcb == 1 and native_z.get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE)
+
+
+def _chain_key(blocks, x):
+    return (tuple(id(b) for b in blocks), tuple(x.shape), x.device, _SOLVE['convergence'],
+            tuple(getattr(b, 'convergence', None) for b in blocks), tuple(int(b.threshold) for b in blocks),
+            tuple(float(b.eps_forward) for b in blocks))
+
+
+def eval_exact_chain(blocks, x, logpx, owner=None):
     """A SequentialFlow of fc imBlocks in eval (train_tabular.py:314-336) in one engine call
     (inf_flow_eval_exact_chain): every block's inf_imblock_eval_exact back to back on the stream, the log-density
     steps on the device.  Returns (z, logpx (B, 1)), or None when a block is not eligible (the caller then runs the
-    blocks one by one; nothing has run)."""
+    blocks one by one; nothing has run).  `owner` (the SequentialFlow) keeps the host-side plan between calls."""
     if (x.dim() != 2 or x.shape[1] > 10 or not x.is_cuda or x.dtype != torch.float32 or not blocks or
             any(not isinstance(b, imBlock) or b.training or b.exact_trace or _needs_graph(b, x) for b in blocks)):
         return None
@@ -269,35 +314,39 @@ def eval_exact_chain(blocks, x, logpx):
     lib = _hip.load()
     x = x.contiguous()
     B, n = x.shape[0], len(blocks)
-    natives = [b._native(x) for b in blocks]
-    stream = natives[0][2]
-    nx = (ctypes.c_void_p * n)(*[p[0].handle.value for p in natives])
-    nz = (ctypes.c_void_p * n)(*[p[1].handle.value for p in natives])
-    T = (ctypes.c_int * n)(*[int(b.threshold) for b in blocks])
-    eps = (ctypes.c_double * n)(*[float(b.eps_forward) for b in blocks])
-    stats = (_hip.BroydenStats * n)()
-    samples = []
-    for i, p in enumerate(natives):
-        if p[1].get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE:
-            arrs = [(ctypes.c_int * B)() for _ in range(3)]
-            stats[i].sample_nstep, stats[i].sample_lowest_step, stats[i].sample_prot_break = [
-                ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in arrs]
-            samples.append(arrs)
-        else:
-            samples.append(None)
-    ws = _hip.workspace(x.device, lib.inf_flow_chain_workspace_bytes(nz, n, B, T))
+    key = _chain_key(blocks, x)
+    plan = owner.__dict__.get('_chain_plan') if owner is not None else None
+    if plan is None or plan[0] != key:
+        # Only where the blocks run as block-kernel launches (INF_OPT_FC_BLOCK): there every block ends in a host
+        # readback, so the host work between blocks leaves the GPU idle, and one call removes it.  On the
+        # launch-per-iteration path a block returns with its z-branch Jacobian still queued, which hides part of the
+        # next block's host work (measured: tools/ab_chain.py).
+        if not _chain_eligible(blocks[0]._native(x)[1]):
+            return None
+        plan = (key, _ChainPlan(blocks, x))
+        if owner is not None:
+            owner.__dict__['_chain_plan'] = plan
+    else:
+        sig = plan[1].signature()
+        if sig != plan[1].sig:                 # weights / u / v changed: the blocks' refresh repacks them
+            for b in blocks:
+                b._native(x)
+            plan[1].sig = plan[1].signature()
+    p = plan[1]
+    if not _chain_eligible(p.natives[0][1]):
+        return None
     z = torch.empty_like(x)
     lp_in = _logp_tensor(logpx, B, x.device)
     lp_out = torch.empty(B, device=x.device)
-    rc = lib.inf_flow_eval_exact_chain(nx, nz, n, _hip.ptr(x), _hip.ptr(z), _hip.ptr(lp_in) if lp_in is not None else None,
-                                       _hip.ptr(lp_out), B, T, eps, stats, _hip.ptr(ws), ws.numel(), stream)
+    rc = lib.inf_flow_eval_exact_chain(p.nx, p.nz, n, _hip.ptr(x), _hip.ptr(z), _hip.ptr(lp_in), _hip.ptr(lp_out), B,
+                                       p.T, p.eps, p.stats, _hip.ptr(p.ws), p.ws.numel(), p.stream)
     if rc == _hip.INF_ERR_UNSUPPORTED:
         return None
     _hip.check(rc, 'inf_flow_eval_exact_chain')
     for i, b in enumerate(blocks):
-        d = stats[i].as_dict(int(b.threshold))
-        if samples[i] is not None:
-            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in samples[i]]
+        d = p.stats[i].as_dict(int(b.threshold))
+        if p.samples[i] is not None:
+            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in p.samples[i]]
         b.last_broyden = d
     return z, lp_out.view(B, 1)
 

@@ -101,21 +101,7 @@ def _prot_break_deep_block():
     return blk.to(DEV).eval()
 
 
-@pytest.mark.parametrize('fc_block', [2, 0], ids=['block_kernel', 'launch_path'])
-@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
-def test_protective_break_on_fused_fc_paths(golden_dir, convergence, fc_block):
-    """prot_break_deep_b6 (the reference on PROT_BREAK_DEEP): global rule -> the batch breaks at step 1 and takes the
-    Banach fixed point; per-sample rule -> the coupled samples break, the samples with x0 == 0 converge in Broyden.
-    prot_break, the Broyden step counts and the fixed-point iteration count exact; z within 2e-5 of its max, per-sample
-    log p within 2e-3 nats, nats within 1e-5."""
-    import os
-    path = os.path.join(golden_dir, 'prot_break_deep_b6.npz')
-    if not os.path.exists(path):
-        pytest.skip('missing fixture prot_break_deep_b6')
-    g = np.load(path)
-    tag = 'g' if convergence == 'global' else 'ps'
-    x = torch.from_numpy(g['x']).to(DEV)
-    torch.testing.assert_close(x.cpu(), syn.prot_break_deep_batch(int(g['seed'])), rtol=0, atol=0)
+def _run_prot_break_deep(x, convergence, fc_block):
     B = x.shape[0]
     blk = _prot_break_deep_block()
     blk.convergence = convergence
@@ -132,8 +118,35 @@ def test_protective_break_on_fused_fc_paths(golden_dir, convergence, fc_block):
         torch.cuda.synchronize()
     finally:
         stats = _hip.profile_end()
-    assert (TAG_BLOCK in {s_['tag'] for s_ in stats}) == bool(fc_block)
-    st = blk.last_broyden
+    return z, lp, blk.last_broyden, {s_['tag'] for s_ in stats}, nets
+
+
+def _load_prot_break_deep(golden_dir):
+    import os
+    path = os.path.join(golden_dir, 'prot_break_deep_b6.npz')
+    if not os.path.exists(path):
+        pytest.skip('missing fixture prot_break_deep_b6')
+    g = np.load(path)
+    x = torch.from_numpy(g['x']).to(DEV)
+    torch.testing.assert_close(x.cpu(), syn.prot_break_deep_batch(int(g['seed'])), rtol=0, atol=0)
+    return g, x
+
+
+@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
+def test_protective_break_fused_fc_launch_path_matches_reference(golden_dir, convergence, monkeypatch):
+    """prot_break_deep_b6 (the reference on PROT_BREAK_DEEP, the POWER nets' shape) on the fused fc launch path with
+    exact fp32 MFMA (fcnet.hip, INFLOW_MFMA=f32): the protective-break branch of inf_imblock_eval_exact (Banach fallback
+    from the solve's buffers, the z recompute, the z-branch Jacobian on the recomputed z).  Global rule -> the batch
+    breaks at step 1 and takes the fixed point; per-sample rule -> the coupled samples break, the samples with x0 == 0
+    converge in Broyden.  prot_break, step counts and the fixed-point iteration count exact; z within 2e-5 of its max,
+    per-sample log p within 2e-3 nats, nats within 1e-5.  (The scaled fp16 split cannot carry this fixture: after the
+    first step an iterate holds 1e-9 and 0.6 in one column, and the split's error is relative to the column's max.)"""
+    g, x = _load_prot_break_deep(golden_dir)
+    tag = 'g' if convergence == 'global' else 'ps'
+    monkeypatch.setenv('INFLOW_MFMA', 'f32')
+    z, lp, st, tags, nets = _run_prot_break_deep(x, convergence, 0)
+    assert all(n.lib.inf_net_get_mfma(n.handle) == 0 for n in nets)
+    assert 601 in tags and TAG_BLOCK not in tags, sorted(tags)
     assert st['prot_break'], st
     fp_ref = g[tag + '_fixed_point_iters']
     assert st['fixed_point_iters'] == int(fp_ref.max()), (st['fixed_point_iters'], fp_ref)
@@ -148,6 +161,23 @@ def test_protective_break_on_fused_fc_paths(golden_dir, convergence, fc_block):
     logpx = (logpz + lp.double().view(-1)).cpu().numpy()
     np.testing.assert_allclose(logpx, g[tag + '_logpx'], rtol=0, atol=2e-3)
     assert abs(-logpx.mean() - float(g[tag + '_nats'])) <= 1e-5
+
+
+@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
+def test_protective_break_block_kernel_matches_launch_path(golden_dir, convergence):
+    """The block kernel's protective-break handling (it reports the break and leaves x, f_x(x), x_embed and the lowest
+    iterates in global memory; the host runs the Banach fallback and the recompute from them) against the launch path on
+    the same f16x3 nets: the same break flags, step counts and fixed-point iterations; z and per-sample log p within
+    2e-5 (the fallback, recompute and z-branch Jacobian are the same launches on both paths)."""
+    g, x = _load_prot_break_deep(golden_dir)
+    zb, lpb, stb, tagsb, _ = _run_prot_break_deep(x, convergence, 2)
+    zl, lpl, stl, tagsl, _ = _run_prot_break_deep(x, convergence, 0)
+    assert TAG_BLOCK in tagsb and TAG_BLOCK not in tagsl
+    assert stb['prot_break'] and stl['prot_break']
+    for k in ('nstep', 'fixed_point_iters', 'sample_prot_break', 'sample_nstep'):
+        assert stb.get(k) == stl.get(k), (k, stb.get(k), stl.get(k))
+    np.testing.assert_allclose(zb.cpu().numpy(), zl.cpu().numpy(), rtol=0, atol=2e-5 * max(1., zl.abs().max().item()))
+    np.testing.assert_allclose(lpb.cpu().numpy(), lpl.cpu().numpy(), rtol=0, atol=2e-5)
 
 
 def test_power_bench_batch_matches_oracle():
@@ -258,6 +288,8 @@ def test_chain_call_matches_block_by_block(convergence, monkeypatch):
     m, _ = _model(arch, B)
     for b in imblocks(m):
         b.convergence = convergence
+    tabular_logpx(m, x)
+    _set_block(m, 2)                     # the chain runs where the blocks are block-kernel launches
     calls = []
     real = imb.eval_exact_chain
 
