@@ -124,9 +124,12 @@ def parse():
     ap.add_argument('--train-step', default='full', choices=['full', 'fwdbwd'],
                     help='train mode: full = forward + backward + clip_grad_norm_(1) + Adam + update_lipschitz + '
                          'EMA (train_img.py:637-658); fwdbwd = forward + backward only')
-    ap.add_argument('--mode', default='eval', choices=['eval', 'train'],
+    ap.add_argument('--mode', default='eval', choices=['eval', 'train', 'trainfwd'],
                     help='eval: the density-evaluation hot path (BASELINE metric); train: one training step '
-                         '(train-mode forward + loss.backward(), train_img.py:611-638; no optimizer step)')
+                         '(train-mode forward + loss.backward(), train_img.py:611-638; no optimizer step); trainfwd: '
+                         'the train-mode forward without gradients (imBlocks in training mode: the power-series '
+                         'log-det with Geom / Poisson series lengths, implicit_block.py:262-322; BASELINE.md\'s '
+                         '"train-mode forward" calibration rows)')
     return ap.parse_args()
 
 
@@ -141,7 +144,7 @@ def host_threads():
     return max(1, n)
 
 
-def cpu_baseline(arch, sd, model, device, nimg, reps=3):
+def cpu_baseline(arch, sd, model, device, nimg, reps=3, training=False):
     """Oracle (CPU restatement, torch fp32, autograd VJPs) timed as BASELINE.md's CPU-baseline plan prescribes --
     N = nproc threads, one warm-up batch, then the median of `reps` batches of `nimg` (images: B = 64, ~45 s each
     on 16 threads; the warm-up batch is 8 images).  Tabular: the bench batch itself.  Also runs the GPU path on the
@@ -151,12 +154,12 @@ def cpu_baseline(arch, sd, model, device, nimg, reps=3):
     torch.set_num_threads(cores)
     image = arch['kind'] == 'conv'
     if image:
-        flow = orc.build(arch, sd, syn.conv_flow_layout(arch))
+        flow = orc.build(arch, sd, syn.conv_flow_layout(arch), training=training)
         batch = lambda n, seed: syn.image_batch(n, arch['input_size'], arch['nvals'], seed=seed)
         run = lambda xb: orc.image_bits_per_dim(flow, xb, arch['nvals'])
         warm_n = min(8, nimg)
     else:
-        flow = orc.build(arch, sd, syn.fc_flow_layout(arch))
+        flow = orc.build(arch, sd, syn.fc_flow_layout(arch), training=training)
         batch = lambda n, seed: syn.tabular_batch(n, arch['d'], seed=seed)
         run = lambda xb: orc.tabular_nats(flow, xb)
         warm_n = nimg
@@ -255,6 +258,8 @@ def main():
     np.random.seed(0)
     torch.manual_seed(0)
 
+    if args.mode == 'trainfwd':
+        model.train()                          # the series log-det of training, evaluated without gradients
     if args.mode == 'train':
         model.train()                          # probes: --probes (device RNG by default, as in eval)
         params = [p for p in model.parameters() if p.requires_grad]
@@ -357,7 +362,8 @@ def main():
     # fp32-equivalent peak of the arithmetic the dominant kernel issues: its algorithmic FLOPs over the time its
     # MFMA instructions take at their dense peak (engine prof peak_ms; frac = MFMA-pipe fraction)
     peak = dom['flops'] / (dom['peak_ms'] * 1e9) if dom.get('peak_ms') else FP32_MFMA_PEAK_TFLOPS
-    what = 'density eval' if args.mode == 'eval' else 'training step'
+    what = {'eval': 'density eval', 'train': 'training step',
+            'trainfwd': 'train-mode forward (power-series log-det, no gradients)'}[args.mode]
     if args.config == 'power':
         workload = ('power: POWER tabular implicit flow %s (run_tabular.sh arch: 20 imBlocks, 6-128x4-6 sin, '
                     'coeff 0.99, exact 6x6 log-det), batch %d per GPU' % (what, B))
@@ -369,6 +375,8 @@ def main():
             args.config, what, '' if args.config == 'cifar10' else ' variant', B)
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
+        ('samples/sec (whole node), %s train-mode forward (power-series log-det, no gradients)' % args.config)
+        if args.mode == 'trainfwd' else
         'samples/sec (whole node), %s training step (%s)' % (
             args.config, 'forward + backward + grad clip + Adam + update_lipschitz + EMA'
             if args.train_step == 'full' else 'forward + backward'),
@@ -383,7 +391,7 @@ def main():
         'config': {'workload': workload,
                    'global_batch': B * world, 'per_gpu_batch': B, 'parallelism': 'dp%d' % world,
                    'dist_backend': (torch.distributed.get_backend() if world > 1 else None),
-                   'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps},
+                   'probes': args.probes, 'broyden_steps': steps_info, 'n_power_series': nps, 'mode': args.mode},
         ('bits_per_dim' if image else 'nats'): round(bpd, 6),
         'roofline': {'bound': 'mfma', 'kernel': _hip.tag_name(dom['tag']), 'achieved': round(achieved, 2),
                      'peak': round(peak, 1), 'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4),
@@ -412,8 +420,9 @@ def main():
                                     for s in stats], key=lambda r: -r['ms'])[:12]},
         'cpu_baseline': None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline and arch_name != 'celebahq256' and args.mode == 'eval':
-        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch if image else B, args.cpu_reps)
+    if rank == 0 and world == 1 and args.cpu_baseline and arch_name != 'celebahq256' and args.mode != 'train':
+        cb, delta, ref_bpd = cpu_baseline(arch, sd, model, device, args.cpu_batch if image else B, args.cpu_reps,
+                                          training=args.mode == 'trainfwd')
         out['cpu_baseline'] = cb
         out['bpd_delta_vs_oracle' if image else 'nats_delta_vs_oracle'] = delta
         out['speedup_vs_cpu_baseline'] = round(value / cb['value'], 1)
