@@ -115,12 +115,17 @@ struct InfNet {
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
   int fc_block = 1;        // INF_OPT_FC_BLOCK (read on net_z of inf_imblock_eval_exact)
+  int fc_series = 1;       // INF_OPT_FC_SERIES (read on the first net of inf_logdet_series[_pair])
   // fused fc path (fcnet.hip): the whole net in one launch per evaluation (forward and forward-mode Jacobian)
   bool fcfused = false;
   // f16x3 planes of the fused fc layers (fcnet_h3.hip, filled at refresh): layer l at fch + fch_off[l], exponent fchexp[l]
   uint16_t* fch = nullptr;
   int* fchexp = nullptr;
   std::vector<size_t> fch_off;
+  // the transposed layers' planes (fcseries_kernel): position j = W_{L-1-j}^T (w.g.A), the same tile shapes as fch's
+  // layer j, at fch_off[j], exponent fchtexp[j]
+  uint16_t* fcht = nullptr;
+  int* fchtexp = nullptr;
 };
 
 namespace {
@@ -1495,12 +1500,14 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
         const int nrt = l == L - 1 ? 1 : 8, nks = l == 0 ? 1 : 4;
         halves += (size_t)nrt * nks * 1024;
       }
-      if (hipMalloc(&n->fch, halves * sizeof(uint16_t)) != hipSuccess ||
-          hipMalloc(&n->fchexp, (size_t)L * sizeof(int)) != hipSuccess) {
+      if (hipMalloc(&n->fch, 2 * halves * sizeof(uint16_t)) != hipSuccess ||
+          hipMalloc(&n->fchexp, 2 * (size_t)L * sizeof(int)) != hipSuccess) {
         if (n->fch) (void)hipFree(n->fch);
         delete n;
         return INF_ERR_HIP;
       }
+      n->fcht = n->fch + halves;            // one allocation each: freed with fch / fchexp
+      n->fchtexp = n->fchexp + L;
       n->mfma_mode = INF_MFMA_F16X3;
       const char* mm = getenv("INFLOW_MFMA");
       if (mm && *mm) {
@@ -1557,7 +1564,8 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     const EnvOpt opts[] = {{"INFLOW_FUSED_K128", &n->k128, k128_v, 3},
                            {"INFLOW_EVAL_OVERLAP", &n->eval_overlap, bin_v, 2},
                            {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2},
-                           {"INFLOW_FC_BLOCK", &n->fc_block, k128_v, 3}};
+                           {"INFLOW_FC_BLOCK", &n->fc_block, k128_v, 3},
+                           {"INFLOW_FC_SERIES", &n->fc_series, bin_v, 2}};
     for (const EnvOpt& o : opts) {
       const char* e = getenv(o.name);
       if (!e || !*e) continue;
@@ -1658,6 +1666,9 @@ int inf_net_refresh(InfNet* n, void* stream) {
       const WLayer& w = n->L[l];
       const int nrt = l == L - 1 ? 1 : 8, nks = l == 0 ? 1 : 4;
       INF_TRY(launch_fc_split_h3(w.f.A, w.cout, w.f.Kpad, nrt, nks, n->fch + n->fch_off[l], n->fchexp + l, s));
+      // transposed position j = L-1-l: rows cin, k = cout (w.g.A = W^T, row stride g.Kpad), position j's tile shape
+      const int j = L - 1 - l, trt = j == L - 1 ? 1 : 8, tks = j == 0 ? 1 : 4;
+      INF_TRY(launch_fc_split_h3(w.g.A, w.cin, w.g.Kpad, trt, tks, n->fcht + n->fch_off[j], n->fchtexp + j, s));
     }
   }
   if (n->fused) {
@@ -2166,15 +2177,58 @@ int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_
   return INF_OK;
 }
 
-int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
-                      int B, void* ws, size_t ws_bytes, void* stream) {
-  if (!n || !x || !vareps || !coeff || !out || B <= 0 || n_terms < 0 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream;
+// The power series of fused f16x3 fc nets in one launch for the pair (fcblock.hip fcseries_kernel; inputs in the
+// boundary layout), when the first net's INF_OPT_FC_SERIES is 1 and a kernel exists for the shape; else
+// INF_ERR_UNSUPPORTED and the caller takes the per-layer path
+static int fc_series(InfNet* const* nets, const float* const* xs, const float* const* es, const float* coeff,
+                     int n_terms, float* const* outs, int nn, int B, hipStream_t s) {
+  if (!nets[0]->fc_series || n_terms < 1) return INF_ERR_UNSUPPORTED;
+  for (int i = 0; i < nn; ++i)
+    if (!nets[i]->fcfused || !nets[i]->fcht || nets[i]->mfma_mode != INF_MFMA_F16X3) return INF_ERR_UNSUPPORTED;
+  FcSeriesArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nn = nn;
+  a.nl = (int)nets[0]->L.size();
+  a.d = nets[0]->d;
+  a.act = nets[0]->L[0].act;
+  a.B = B;
+  a.n_terms = n_terms;
+  for (int k = 0; k < n_terms; ++k) a.coeff[k] = coeff[k];
+  for (int i = 0; i < nn; ++i) {
+    const InfNet* n = nets[i];
+    if ((int)n->L.size() != a.nl || n->d != a.d || n->L[0].act != a.act || a.nl > FC_MAXL) return INF_ERR_UNSUPPORTED;
+    for (int l = 0; l < a.nl; ++l) {
+      FcLayer& f = a.f[i].L[l];
+      f.A = n->L[l].f.A;
+      f.Ah = n->fch + n->fch_off[l];
+      f.Aexp = n->fchexp + l;
+      f.Kpad = n->L[l].f.Kpad;
+      f.b = n->L[l].b;
+      f.beta = n->L[l].act_beta;
+      FcLayer& t = a.t[i].L[l];
+      t.Ah = n->fcht + n->fch_off[l];
+      t.Aexp = n->fchtexp + l;
+    }
+    a.x[i] = xs[i];
+    a.eps[i] = es[i];
+    a.out[i] = outs[i];
+  }
+  return launch_fcseries(a, s);
+}
+
+// try_fc: the one-launch fc series first (inf_logdet_series); the pair's per-net fallback has already asked the first net
+static int series_single(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
+                         int B, void* ws, size_t ws_bytes, hipStream_t s, bool try_fc) {
   Bufs bf;
   if (!ws || carve(n, B, 1, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
   if (n_terms == 0) {
     INF_HIP(hipMemsetAsync(out, 0, sizeof(float) * B, s));
     return INF_OK;
+  }
+  if (try_fc) {
+    InfNet* nets1[1] = {n};
+    const int st = fc_series(nets1, &x, &vareps, coeff, n_terms, &out, 1, B, s);
+    if (st != INF_ERR_UNSUPPORTED) return st;
   }
   int st = INF_OK;
   const float* xi = to_internal(n, x, bf.xin, B, s, &st);
@@ -2192,6 +2246,12 @@ int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const floa
   return launch_series_combine(bf.part, coeff, n_terms, B, bf.nchunk, out, s);
 }
 
+int inf_logdet_series(InfNet* n, const float* x, const float* vareps, const float* coeff, int n_terms, float* out,
+                      int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !vareps || !coeff || !out || B <= 0 || n_terms < 0 || n_terms > SERIES_MAX) return INF_ERR_INVALID;
+  return series_single(n, x, vareps, coeff, n_terms, out, B, ws, ws_bytes, (hipStream_t)stream, true);
+}
+
 // Both log-det series of an imBlock (x-branch and z-branch, implicit_block.py:318-322) advanced in
 // lockstep: when both nets take the fused path, every term is ONE launch over both nets' tiles.
 // ws must hold 2 x inf_workspace_bytes(net, batch, 1).
@@ -2204,9 +2264,17 @@ int inf_logdet_series_pair(InfNet* na, const float* xa, const float* ea, InfNet*
   const size_t half = ws_need(na, B, 1);
   if (!ws || ws_bytes < 2 * half) return INF_ERR_WORKSPACE;
   char* w0 = reinterpret_cast<char*>(ws);
+  if (n_terms > 0) {
+    InfNet* nets2[2] = {na, nb};
+    const float* xs2[2] = {xa, xb};
+    const float* es2[2] = {ea, eb};
+    float* outs2[2] = {out_a, out_b};
+    const int st = fc_series(nets2, xs2, es2, coeff, n_terms, outs2, 2, B, (hipStream_t)stream);
+    if (st != INF_ERR_UNSUPPORTED) return st;
+  }
   if (!(na->fused && nb->fused && na->fhid == nb->fhid)) {
-    INF_TRY(inf_logdet_series(na, xa, ea, coeff, n_terms, out_a, B, w0, half, stream));
-    return inf_logdet_series(nb, xb, eb, coeff, n_terms, out_b, B, w0 + half, half, stream);
+    INF_TRY(series_single(na, xa, ea, coeff, n_terms, out_a, B, w0, half, (hipStream_t)stream, false));
+    return series_single(nb, xb, eb, coeff, n_terms, out_b, B, w0 + half, half, (hipStream_t)stream, false);
   }
   hipStream_t s = (hipStream_t)stream;
   Bufs bfa, bfb;
@@ -2622,6 +2690,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
     case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;
     case INF_OPT_FC_BLOCK: slot = &n->fc_block; hi = 2; break;
+    case INF_OPT_FC_SERIES: slot = &n->fc_series; hi = 1; break;
     default: return -INF_ERR_INVALID;
   }
   if (value < lo || value > hi) return -INF_ERR_INVALID;
@@ -2640,6 +2709,7 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_CONVERGENCE: return n->convergence;
     case INF_OPT_K128_EXACT_SCALE: return n->exact_scale;
     case INF_OPT_FC_BLOCK: return n->fc_block;
+    case INF_OPT_FC_SERIES: return n->fc_series;
     default: return -INF_ERR_INVALID;
   }
 }

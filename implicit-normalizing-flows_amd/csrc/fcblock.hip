@@ -168,6 +168,13 @@ __device__ __forceinline__ void load_net(const FcArgs& a, int w, int lane, u32x4
   r.wo = lds_w + BK_W0_VEC;
 }
 
+// the activation derivatives a forward pass saves for the VJP passes of the power series (mlp_pass SV modes)
+enum { SV_NONE = 0, SV_SAVE = 1, SV_VJP = 2 };
+template <int NH, int NCB>
+struct Derivs {
+  float d[NH + 1][NCB][4];
+};
+
 // LDS scratch of one pass over NC columns
 struct Pass {
   uint16_t* pl0;   // [col][k] h plane
@@ -223,9 +230,13 @@ __device__ __forceinline__ void split_input(const Pass& P) {
 // (no bias) left in tmp rows [0, 16).  The arithmetic of fcnet_h3.hip per column: scaled two-piece fp16 operands, three
 // products per fp32 product on v_mfma_f32_16x16x32_f16, fp32 accumulation, exact unscale.  JAC: column block 0 is the
 // primal, the others are tangents, multiplied by act'(pre-activation of the primal).  REG: the weights come from
-// registers (loaded once per solve) instead of global memory.
-template <int NCB, bool JAC, int ACT, int NH, bool REG>
-__device__ __forceinline__ void mlp_pass(const FcArgs& a, const NetRegs<NH>* R, const Pass& P, Stamps* ts) {
+// registers (loaded once per solve) instead of global memory.  SV_SAVE: a forward pass that also keeps act' of
+// every hidden unit in D (registers: wave w holds rows 16 w + 4 g + r of every hidden layer); SV_VJP: the pass of the
+// transposed net (a.L[j] = W_{L-1-j}^T, fcseries_kernel) whose hidden epilogue is the product with D's derivatives of
+// forward layer NH - j instead of bias + activation -- the row ownership of both passes is the same.
+template <int NCB, bool JAC, int ACT, int NH, bool REG, int SV = SV_NONE, class NA = FcArgs>
+__device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, const Pass& P, Stamps* ts,
+                                         Derivs<NH, NCB>* D = nullptr) {
   constexpr int NC = 16 * NCB;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -244,8 +255,10 @@ __device__ __forceinline__ void mlp_pass(const FcArgs& a, const NetRegs<NH>* R, 
     constexpr int NKS = decltype(nksc)::value;
     const FcLayer& L = a.L[l];
     float bias[4];
+    if constexpr (SV != SV_VJP) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
+      for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
+    }
     f32x4 acc[NCB];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -259,7 +272,7 @@ __device__ __forceinline__ void mlp_pass(const FcArgs& a, const NetRegs<NH>* R, 
         acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
       }
     const int sw = ldc(L.Aexp);
-    const float sp = (ACT == ACT_SWISH) ? softplus_f(ldc(L.beta)) : 0.f;
+    const float sp = (ACT == ACT_SWISH && SV != SV_VJP) ? softplus_f(ldc(L.beta)) : 0.f;
     float v[NCB][4];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
@@ -269,7 +282,13 @@ __device__ __forceinline__ void mlp_pass(const FcArgs& a, const NetRegs<NH>* R, 
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if constexpr (JAC) {
+      if constexpr (SV == SV_VJP) {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) v[cb][r] *= D->d[NH - l][cb][r];
+      } else if constexpr (SV == SV_SAVE) {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) bk_act_fd<ACT>(v[cb][r] + bias[r], sp, v[cb][r], D->d[l][cb][r]);
+      } else if constexpr (JAC) {
         const float z = v[0][r] + bias[r];
         float dd;
         bk_act_fd<ACT>(z, sp, v[0][r], dd);
@@ -1054,6 +1073,87 @@ __global__ __launch_bounds__(BK_NT) void fcblock_kernel(FcBlockArgs a) {
   }
   if (err || prot) return;
   }  // jp
+}
+
+// ---- the power-series log-det of a fused fc net pair (basic_logdet_estimator, implicit_block.py:418-426) ----------------
+// Workgroup (blockIdx.x, net blockIdx.y) owns 48 samples: one forward pass of f at x keeps act' of every hidden unit in
+// registers (SV_SAVE), then term k = 1 .. n: v <- v^T J_f(x) as one pass of the transposed net over the 48 columns
+// (SV_VJP: the hidden epilogue multiplies by the saved derivatives), tr_k = v . eps (fp64 sum of the d products), and
+// logdet += fl(c_k * (float) tr_k) in fp32 in k order (launch_series_combine's arithmetic).  The operands stay in LDS and
+// registers between terms; the only global traffic is x, eps, the out row and the weight planes (L2-resident).
+constexpr int FS_LDS = 2 * 2 * BK_S * BK_LD + 4 * 16 * BK_S + 4 * BK_NW * BK_S + 4 * BK_S + 64;
+template <int DD, int ACT, int NH>
+__global__ __launch_bounds__(BK_NT) void fcseries_kernel(FcSeriesArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[FS_LDS];
+  const int tid = threadIdx.x, net = blockIdx.y;
+  const long b0 = (long)blockIdx.x * BK_S;
+  const int B = a.B;
+  const Pass P = bk_pass(lds, BK_S);
+  const float* x = a.x[net];
+  const float* ep = a.eps[net];
+  for (int i = tid; i < 16 * BK_S; i += BK_NT) {
+    const int k = i / BK_S, c = i - k * BK_S;
+    P.tmp[i] = (k < DD && b0 + c < B) ? x[(b0 + c) * DD + k] : 0.f;
+  }
+  Derivs<NH, BK_FCB> D;
+  mlp_pass<BK_FCB, false, ACT, NH, false, SV_SAVE>(a.f[net], nullptr, P, nullptr, &D);
+  float ev[DD];
+  const bool mine = tid < BK_S && b0 + tid < B;
+#pragma unroll
+  for (int i = 0; i < DD; ++i) ev[i] = mine ? ep[(b0 + tid) * DD + i] : 0.f;
+  for (int i = tid; i < 16 * BK_S; i += BK_NT) {   // after mlp_pass's last barrier: nobody reads f(x)
+    const int k = i / BK_S, c = i - k * BK_S;
+    P.tmp[i] = (k < DD && b0 + c < B) ? ep[(b0 + c) * DD + k] : 0.f;
+  }
+  float acc = 0.f;
+  for (int k = 0; k < a.n_terms; ++k) {
+    mlp_pass<BK_FCB, false, ACT, NH, false, SV_VJP>(a.t[net], nullptr, P, nullptr, &D);
+    if (tid < BK_S) {      // rows >= DD of the VJP are zero (the transposed output planes' padding rows)
+      double tr = 0.0;
+#pragma unroll
+      for (int i = 0; i < DD; ++i) tr += (double)P.tmp[i * BK_S + tid] * (double)ev[i];
+      acc = acc + a.coeff[k] * (float)tr;
+    }
+  }
+  if (mine) a.out[net][b0 + tid] = acc;
+}
+
+int fcseries_supported(const FcSeriesArgs& a) {
+  if (a.nn < 1 || a.nn > 2 || a.B <= 0 || a.n_terms < 1 || a.n_terms > 128) return 0;
+  const int nh = a.nl - 2;
+  if (!((a.d == 6 && nh == 3) || (a.d == 2 && nh == 1))) return 0;
+  if (a.act != ACT_SIN && a.act != ACT_SWISH) return 0;
+  for (int i = 0; i < a.nn; ++i) {
+    if (!a.x[i] || !a.eps[i] || !a.out[i]) return 0;
+    for (int l = 0; l < a.nl; ++l)
+      if (!a.f[i].L[l].Ah || !a.f[i].L[l].Aexp || !a.t[i].L[l].Ah || !a.t[i].L[l].Aexp) return 0;
+  }
+  return 1;
+}
+
+int launch_fcseries(const FcSeriesArgs& a, hipStream_t s) {
+  if (!fcseries_supported(a)) return INF_ERR_UNSUPPORTED;
+  const int nh = a.nl - 2;
+  const dim3 grid((unsigned)fcblock_grid(a.B), (unsigned)a.nn);
+  const bool prof = prof_enabled();
+  if (prof) prof_begin_launch(s);
+#define FS_GO(DD_, ACT_, NH_) hipLaunchKernelGGL((fcseries_kernel<DD_, ACT_, NH_>), grid, dim3(BK_NT), 0, s, a)
+  if (a.d == 6 && nh == 3) {
+    if (a.act == ACT_SIN) FS_GO(6, ACT_SIN, 3);
+    else FS_GO(6, ACT_SWISH, 3);
+  } else {
+    if (a.act == ACT_SIN) FS_GO(2, ACT_SIN, 1);
+    else FS_GO(2, ACT_SWISH, 1);
+  }
+#undef FS_GO
+  INF_CHECK_LAUNCH();
+  if (prof) {
+    // flops: the forward pass and n_terms transposed passes per sample and net
+    const double per_eval = 2.0 * a.d * FC_H * 2 + (double)nh * 2.0 * FC_H * FC_H;
+    const double f = per_eval * a.B * a.nn * (1.0 + a.n_terms);
+    prof_end_launch(s, 620, f, 4.0 * a.B * a.nn * (3.0 * a.d + 1.0), 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+  }
+  return INF_OK;
 }
 
 size_t fcblock_lds_bytes(int d, int T) { return bk_layout(d, T).total; }

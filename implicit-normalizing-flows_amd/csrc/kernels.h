@@ -289,6 +289,25 @@ size_t fcblock_lds_bytes(int d, int T);
 // INF_ERR_UNSUPPORTED when the configuration has no kernel or (global rule) the grid cannot be co-resident
 int launch_fcblock(const FcBlockArgs& a, hipStream_t s);
 
+// the power-series log-det of fused fc nets in one launch (fcblock.hip fcseries_kernel; basic_logdet_estimator,
+// implicit_block.py:418-426): per workgroup of 48 samples, one forward pass keeping act' in registers, then the n_terms
+// VJPs v <- v^T J through the transposed net's planes, each dotted with the probe and combined like
+// launch_series_combine (fl(c_k * (float) dot) accumulated in fp32 in k order)
+struct FcPlanes {
+  FcLayer L[FC_MAXL];
+};
+struct FcSeriesArgs {
+  FcPlanes f[2];          // the nets' forward layers (f16x3 planes, exponents, biases, Swish beta)
+  FcPlanes t[2];          // their transposed layers: t.L[j] = W_{nl-1-j}^T planes and exponents
+  const float* x[2];      // (B, d) boundary layout
+  const float* eps[2];    // (B, d) probes
+  float* out[2];          // (B)
+  float coeff[128];       // c_k, k < n_terms
+  int nn, nl, d, act, B, n_terms;
+};
+int fcseries_supported(const FcSeriesArgs& a);
+int launch_fcseries(const FcSeriesArgs& a, hipStream_t s);
+
 // ------------------------------------------------------------------------------------------
 // parameter gradients (grad.hip)
 // ------------------------------------------------------------------------------------------

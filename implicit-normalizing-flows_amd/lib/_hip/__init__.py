@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
 INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE, INF_OPT_K128_EXACT_SCALE = 1, 2, 3, 4   # InfNetOption
-INF_OPT_FC_BLOCK = 5
+INF_OPT_FC_BLOCK, INF_OPT_FC_SERIES = 5, 6
 INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
 CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 
@@ -372,6 +372,10 @@ def tag_name(tag):
                                  ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
     if tag in (600, 601):    # fused fc net (fcnet.hip): forward + fc_out epilogue / forward-mode Jacobian + LU
         return 'fcnet_kernel<%s>' % ('FWD', 'JAC')[tag - 600]
+    if tag == 610:           # one launch per fc imBlock evaluation (fcblock.hip)
+        return 'fcblock_kernel'
+    if tag == 620:           # the power series of an fc net pair in one launch (fcblock.hip)
+        return 'fcseries_kernel'
     if tag == 899:
         return 'wgrad_valu_kernel'
     if 800 <= tag < 900:     # weight-gradient kernel (grad.hip), 8<TMW><TNW>

@@ -668,18 +668,19 @@ class imBlock(nn.Module):
                     for a, b in zip(dsts, srcs):
                         a.copy_(b)
 
-    def _host_scalar(self, name, t):
-        """t.item() without a device sync per call: re-read only when the tensor changed."""
+    def _host_scalar(self, name, t, fn=None):
+        """fn(t).item() without a device sync per call: re-read only when the tensor changed."""
         key = (t.data_ptr(), t._version, t.device)
         cache = self.__dict__.setdefault('_host_scalars', {})
         if cache.get(name, (None,))[0] != key:
-            cache[name] = (key, t.item())
+            with torch.no_grad():
+                cache[name] = (key, (fn(t) if fn is not None else t).item())
         return cache[name][1]
 
     def _series_plan(self):
         """Series length and coefficient function (implicit_block.py:261-289)."""
         if self.n_dist == 'geometric':
-            param = torch.sigmoid(self.geom_p).item()
+            param = self._host_scalar('geom_p', self.geom_p, torch.sigmoid)   # torch.sigmoid(geom_p).item()
         elif self.n_dist == 'poisson':
             param = self._host_scalar('lamb', self.lamb)
         else:

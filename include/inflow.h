@@ -142,14 +142,19 @@ int inf_net_get_mfma(const InfNet* net);
  *                         the launch, the host reading the statistics once.  0 never; 1 (default; INFLOW_FC_BLOCK at
  *                         create) for the per-sample rule only, where it is the faster path; 2 for both rules.
  *                         Otherwise every net evaluation is a launch and the host reads each iteration's norm.
- * Unknown values of INFLOW_FUSED_K128 / INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP (0/1) and INFLOW_CONVERGENCE (global/per_sample)
+ *   INF_OPT_FC_SERIES     read on the first net of inf_logdet_series / inf_logdet_series_pair: 1 (default;
+ *                         INFLOW_FC_SERIES at create) runs the power series of fused f16x3 fc nets (d = 6 with 3 hidden
+ *                         layers or d = 2 with 1) as one launch for both nets: one forward pass keeping act' in registers,
+ *                         then every term's VJP through the transposed weights' planes, dotted with the probe in the same
+ *                         launch; 0 runs one GEMM launch per layer and term.
+ * Unknown values of INFLOW_FUSED_K128 / INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP / INFLOW_FC_SERIES (0/1) and INFLOW_CONVERGENCE (global/per_sample)
  * make inf_net_create fail with INF_ERR_INVALID.
  * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
  * runs the VJP as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322); results
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
   INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4,
-  INF_OPT_FC_BLOCK = 5
+  INF_OPT_FC_BLOCK = 5, INF_OPT_FC_SERIES = 6
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);
