@@ -85,6 +85,17 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
+def all_source_sha():
+    """Hash of every engine source (the phases' kernels live in pointwise.hip / glue.hip / engine.hip)."""
+    h = hashlib.sha256()
+    d = os.path.join(PKG, 'csrc')
+    for f in sorted(os.listdir(d)):
+        if f.endswith(('.hip', '.h')):
+            with open(os.path.join(d, f), 'rb') as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 MFMA_DESC = {
     'bf16x6': 'bf16x6: fp32 operands split exactly into 3 bf16 pieces, 6 products per fp32 product, fp32 '
               'accumulation (error at fp32 level, tests/test_gpu_parity.py::test_split_bf16_error_at_fp32_level)',
@@ -131,6 +142,67 @@ def parse():
                          'log-det with Geom / Poisson series lengths, implicit_block.py:262-322; BASELINE.md\'s '
                          '"train-mode forward" calibration rows)')
     return ap.parse_args()
+
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+# BASELINE.md's HBM-bound phases: the Broyden solve's update / residual kernels and the Hutchinson series' probe draw
+# and term combine (the probe dots themselves are fused into the VJP kernels' epilogues)
+PHASES = (('broyden', (700, 701, 702, 703, 704, 705, 706, 710, 711, 712, 713, 714, 715)), ('hutchinson', (720, 721)))
+
+
+def hbm_phases(stats, config, batch):
+    """roofline.phases: per HBM-bound phase and kernel, the HIP-event time of the profiling step, algorithmic bytes
+    (INF_PROF_LAUNCH's per-launch count) over it as GB/s and as a fraction of 8 TB/s, and -- when
+    profiles/pmc_phases.json holds rocprofv3 FETCH_SIZE / WRITE_SIZE passes for this config and batch -- the measured
+    HBM bytes per dispatch (2 FETCH_SIZE + WRITE_SIZE, x 1024; gfx950's FETCH correction) over the same time."""
+    pmc, src = {}, None
+    path = os.path.join(REPO, 'profiles', 'pmc_phases.json')
+    key = '%s_b%d' % (config, batch)
+    if os.path.exists(path):
+        try:
+            rec = json.load(open(path)).get(key)
+            if rec:
+                pmc = rec['kernels']
+                src = 'profiles/pmc_phases.json[%s] (%s; kernel sources %s)' % (
+                    key, rec.get('measured', '?'),
+                    'as measured' if rec.get('kernel_source_sha') == all_source_sha() else 'changed since')
+        except Exception:
+            pmc = {}
+    by_tag = {s['tag']: s for s in stats}
+    out = {}
+    for phase, tags in PHASES:
+        rows = []
+        for t in tags:
+            st = by_tag.get(t)
+            if not st or st['launches'] == 0 or st['total_ms'] <= 0:
+                continue
+            name = _hip.tag_name(t)
+            row = {'kernel': name, 'launches': st['launches'], 'ms': round(st['total_ms'], 4),
+                   'avg_us': round(st['total_ms'] / st['launches'] * 1e3, 2),
+                   'bytes_per_launch': round(st['bytes'] / st['launches']),
+                   'GBs': round(st['bytes'] / (st['total_ms'] * 1e-3) / 1e9, 1)}
+            row['frac'] = round(row['GBs'] / HBM_PEAK_GBS, 4)
+            if name in pmc:
+                hbm = pmc[name]['hbm_bytes_per_dispatch']
+                row['traffic_per_launch'] = round(hbm)
+                row['traffic_GBs'] = round(hbm * st['launches'] / (st['total_ms'] * 1e-3) / 1e9, 1)
+                row['traffic_frac'] = round(row['traffic_GBs'] / HBM_PEAK_GBS, 4)
+            rows.append(row)
+        if not rows:
+            continue
+        ms = sum(r['ms'] for r in rows)
+        by = sum(r['bytes_per_launch'] * r['launches'] for r in rows)
+        ph = {'ms': round(ms, 4), 'launches': sum(r['launches'] for r in rows),
+              'GBs': round(by / (ms * 1e-3) / 1e9, 1), 'kernels': rows}
+        ph['frac'] = round(ph['GBs'] / HBM_PEAK_GBS, 4)
+        if all('traffic_per_launch' in r for r in rows):
+            tb = sum(r['traffic_per_launch'] * r['launches'] for r in rows)
+            ph['traffic_GBs'] = round(tb / (ms * 1e-3) / 1e9, 1)
+            ph['traffic_frac'] = round(ph['traffic_GBs'] / HBM_PEAK_GBS, 4)
+        out[phase] = ph
+    out['basis'] = ('HIP events around each launch of the profiling step (sequential schedule); GBs = algorithmic '
+                    'bytes / time, frac of %.0f GB/s; traffic from %s' % (HBM_PEAK_GBS, src or 'no PMC record'))
+    return out
 
 
 def host_threads():
@@ -356,6 +428,8 @@ def main():
         except Exception:
             traffic = None
 
+    phases = hbm_phases(stats, arch_name, B)
+
     if torch.is_tensor(bpd):
         bpd = float(bpd)
     mm = mfma_mode()
@@ -400,7 +474,7 @@ def main():
                                     '3 in f16x3 phases; f32 %.1f TF)' % (BF16_MFMA_PEAK_TFLOPS, FP32_MFMA_PEAK_TFLOPS)),
                      'flops_basis': 'algorithmic fp32 FLOPs of the net (2 per multiply-add), not MFMA instruction FLOPs',
                      'traffic': traffic, 'avg_launch_ms': round(avg_ms, 4), 'launches_per_step': dom['launches'],
-                     'traffic_source': traffic_src,
+                     'traffic_source': traffic_src, 'phases': phases,
                      'algorithmic_bytes_per_launch': dom['bytes'] / dom['launches'],
                      'schedule': ('per-kernel durations from one extra step on the sequential eval schedule (timed '
                                   'steps: %s)' % ('x-branch series on a side stream' if overlap_on else 'sequential'))

@@ -216,6 +216,17 @@ void set_hip_error(hipError_t e);
     }                                                   \
   } while (0)
 
+// One profiled launch (inf_profile_begin / _end): the launch between two HIP events on its stream, with its tag and its
+// algorithmic bytes (what the kernel must read and write once; bench.py's roofline.phases)
+#define INF_PROF_LAUNCH(S_, TAG_, BYTES_, ...)          \
+  do {                                                \
+    const bool pr_ = prof_enabled();                  \
+    if (pr_) prof_begin_launch(S_);                   \
+    hipLaunchKernelGGL(__VA_ARGS__);                  \
+    INF_CHECK_LAUNCH();                               \
+    if (pr_) prof_end_launch(S_, TAG_, 0.0, BYTES_);  \
+  } while (0)
+
 #define INF_TRY(expr)                                   \
   do {                                                  \
     int _s = (expr);                                    \

@@ -158,8 +158,7 @@ int glue_normal_logprob(const float* z, float* out, int B, int per, hipStream_t 
 }
 int glue_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, hipStream_t s) {
   if (n == 0) return INF_OK;
-  hipLaunchKernelGGL(rademacher_kernel, GRID1(n), 0, s, out, n, seed, offset);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 721, 4.0 * n, rademacher_kernel, GRID1(n), 0, s, out, n, seed, offset);
   return INF_OK;
 }
 int glue_fixed_point_check(const float* x, const float* xp, const float* y, long n, float eps, unsigned int* count,
@@ -208,8 +207,7 @@ __global__ void recomp_kernel(const float* fx, const float* fz, const float* x, 
 }
 // z = (nnet_x(x) - nnet_z(z*)) + x from the stored net outputs (implicit_block.py:227)
 int glue_recomp(const float* fx, const float* fz, const float* x, float* out, long n, hipStream_t s) {
-  hipLaunchKernelGGL(recomp_kernel, GRID1(n), 0, s, fx, fz, x, out, n);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 706, 16.0 * n, recomp_kernel, GRID1(n), 0, s, fx, fz, x, out, n);
   return INF_OK;
 }
 

@@ -125,9 +125,8 @@ __global__ __launch_bounds__(OUT_CH) void resid_bcast_kernel(const float* f0, co
 }
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s) {
-  hipLaunchKernelGGL(resid_bcast_kernel, dim3(out_nchunk(per), batch), dim3(OUT_CH), 0, s, f0, xemb, z, g, fcur,
-                     partial, per, nchunk);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 700, 16.0 * batch * per + 4.0 * per, resid_bcast_kernel, dim3(out_nchunk(per), batch),
+                  dim3(OUT_CH), 0, s, f0, xemb, z, g, fcur, partial, per, nchunk);
   return INF_OK;
 }
 
@@ -176,16 +175,14 @@ __global__ __launch_bounds__(256) void broyden_start_fc_kernel(const float* f0, 
 }
 int launch_broyden_start_fc(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
                             float* upd, float* x1, float* dx, int batch, int d, hipStream_t s) {
-  hipLaunchKernelGGL(broyden_start_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, f0, xemb, x0, g, fcur,
-                     partial, upd, x1, dx, batch, d);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 702, 28.0 * batch * d + 8.0 * batch, broyden_start_fc_kernel, dim3((batch + 255) / 256),
+                  dim3(256), 0, s, f0, xemb, x0, g, fcur, partial, upd, x1, dx, batch, d);
   return INF_OK;
 }
 int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                           int batch, int d, hipStream_t s) {
-  hipLaunchKernelGGL(resid_bcast_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, f0, xemb, z, g, fcur, partial,
-                     batch, d);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 701, 16.0 * batch * d + 8.0 * batch, resid_bcast_fc_kernel, dim3((batch + 255) / 256),
+                  dim3(256), 0, s, f0, xemb, z, g, fcur, partial, batch, d);
   return INF_OK;
 }
 
@@ -309,8 +306,7 @@ __global__ void axpy_step_kernel(const float* x, const float* upd, float* xnew, 
   dx[i] = xe - x0;
 }
 int launch_axpy_step(const float* x, const float* upd, float* xnew, float* dx, long n, hipStream_t s) {
-  hipLaunchKernelGGL(axpy_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, xnew, dx, n);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 703, 16.0 * n, axpy_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, xnew, dx, n);
   return INF_OK;
 }
 __global__ void neg_kernel(const float* x, float* y, long n) {
@@ -318,8 +314,7 @@ __global__ void neg_kernel(const float* x, float* y, long n) {
   if (i < n) y[i] = -x[i];
 }
 int launch_neg(const float* x, float* y, long n, hipStream_t s) {
-  hipLaunchKernelGGL(neg_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, y, n);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 704, 8.0 * n, neg_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, y, n);
   return INF_OK;
 }
 
@@ -331,9 +326,8 @@ __global__ void reduce_partials_kernel(const double* partial, int batch, int nch
   out[b] = s;
 }
 int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, partial, batch, nchunk,
-                     out);
-  INF_CHECK_LAUNCH();
+  INF_PROF_LAUNCH(s, 705, 8.0 * batch * nchunk + 8.0 * batch, reduce_partials_kernel, dim3((batch + 255) / 256),
+                  dim3(256), 0, s, partial, batch, nchunk, out);
   return INF_OK;
 }
 
@@ -681,13 +675,16 @@ __global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, int
 
 int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   if (a.T > BR_TMAX || a.m >= a.T || a.ncols > a.T) return INF_ERR_INVALID;
+  // algorithmic bytes (fp32, D = batch x d): each kernel's distinct reads and writes of the d-vectors and U / VT columns
+  const double D4 = 4.0 * a.batch * a.d;
   if (a.d <= 32) {
+    // dx, dg, gx, x; U_j, VT_j for j < ncols, j != m; writes U_m, VT_m, update, x_new, dx_new
+    const double by = D4 * (9.0 + 2.0 * (a.ncols > 0 ? a.ncols - 1 : 0));
     const dim3 g((a.batch + 255) / 256);
-    if (a.d == 2) hipLaunchKernelGGL(broyden_small_d_kernel<2>, g, dim3(256), 0, s, a);
-    else if (a.d == 6) hipLaunchKernelGGL(broyden_small_d_kernel<6>, g, dim3(256), 0, s, a);
-    else if (a.d == 8) hipLaunchKernelGGL(broyden_small_d_kernel<8>, g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(broyden_small_kernel, g, dim3(256), 0, s, a);
-    INF_CHECK_LAUNCH();
+    if (a.d == 2) INF_PROF_LAUNCH(s, 715, by, broyden_small_d_kernel<2>, g, dim3(256), 0, s, a);
+    else if (a.d == 6) INF_PROF_LAUNCH(s, 715, by, broyden_small_d_kernel<6>, g, dim3(256), 0, s, a);
+    else if (a.d == 8) INF_PROF_LAUNCH(s, 715, by, broyden_small_d_kernel<8>, g, dim3(256), 0, s, a);
+    else INF_PROF_LAUNCH(s, 715, by, broyden_small_kernel, g, dim3(256), 0, s, a);
     return INF_OK;
   }
   const int nchunk = (a.d + BR_CH - 1) / BR_CH;
@@ -696,19 +693,25 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   double* part3 = part2 + (long)a.batch * nchunk;
   const bool pre = nchunk >= 32;       // (small nchunk: the consumers' own sums are cheaper than three more launches)
   const int nsum = pre ? 1 : nchunk;
+  const double P8 = 8.0 * a.batch * nchunk;   // one fp64 partial per (sample, chunk)
   if (a.m > 0) {
-    hipLaunchKernelGGL(broyden_p1, grid, dim3(256), 0, s, a, nchunk);
-    INF_CHECK_LAUNCH();
-    if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, 2 * a.m), dim3(64), 0, s, a.part, nchunk, 2 * a.T, a.m, a.T, 2 * a.m, a.active);
+    // a_j = dx.U_j, c_j = VT_j.dg: dx, dg, U_j, VT_j (j < m)
+    INF_PROF_LAUNCH(s, 710, D4 * (2.0 + 2.0 * a.m) + P8 * 2 * a.m, broyden_p1, grid, dim3(256), 0, s, a, nchunk);
+    if (pre)
+      INF_PROF_LAUNCH(s, 714, P8 * 2 * a.m + 8.0 * a.batch * 2 * a.m, br_sum_chunks, dim3(a.batch, 2 * a.m), dim3(64),
+                      0, s, a.part, nchunk, 2 * a.T, a.m, a.T, 2 * a.m, a.active);
   }
-  hipLaunchKernelGGL(broyden_p2, grid, dim3(256), 0, s, a, nchunk, nsum, part2);
-  INF_CHECK_LAUNCH();
-  if (pre) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, 1), dim3(64), 0, s, part2, nchunk, 1, 1, 0, 1, a.active);
-  hipLaunchKernelGGL(broyden_p3, grid, dim3(256), 0, s, a, nchunk, nsum, part2, part3);
-  INF_CHECK_LAUNCH();
-  if (pre && a.ncols > 0) hipLaunchKernelGGL(br_sum_chunks, dim3(a.batch, a.ncols), dim3(64), 0, s, part3, nchunk, a.T, a.ncols, 0, a.ncols, a.active);
-  hipLaunchKernelGGL(broyden_p4, grid, dim3(256), 0, s, a, nchunk, nsum, part3);
-  INF_CHECK_LAUNCH();
+  // VT_m, U_m and the denominator: dx, dg, U_j, VT_j (j < m); writes U_m, VT_m
+  INF_PROF_LAUNCH(s, 711, D4 * (4.0 + 2.0 * a.m) + P8, broyden_p2, grid, dim3(256), 0, s, a, nchunk, nsum, part2);
+  if (pre) INF_PROF_LAUNCH(s, 714, P8 + 8.0 * a.batch, br_sum_chunks, dim3(a.batch, 1), dim3(64), 0, s, part2, nchunk, 1, 1, 0, 1, a.active);
+  // scale U_m (read / write U_m, VT_m) and e_j = VT_j.gx: VT_j (j < ncols, j != m), gx
+  INF_PROF_LAUNCH(s, 712, D4 * (4.0 + a.ncols) + P8 * a.ncols, broyden_p3, grid, dim3(256), 0, s, a, nchunk, nsum,
+                  part2, part3);
+  if (pre && a.ncols > 0)
+    INF_PROF_LAUNCH(s, 714, P8 * a.ncols + 8.0 * a.batch * a.ncols, br_sum_chunks, dim3(a.batch, a.ncols), dim3(64), 0,
+                    s, part3, nchunk, a.T, a.ncols, 0, a.ncols, a.active);
+  // update = -(-gx + sum_j e_j U_j), x_new, dx_new: gx, x, U_j (j < ncols); writes update, x_new, dx_new
+  INF_PROF_LAUNCH(s, 713, D4 * (5.0 + a.ncols), broyden_p4, grid, dim3(256), 0, s, a, nchunk, nsum, part3);
   return INF_OK;
 }
 
@@ -1162,8 +1165,9 @@ int launch_series_combine(const double* partials, const float* coeff_host, int n
   if (n_terms > 128) return INF_ERR_UNSUPPORTED;
   CoeffTable ct;
   for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
-  hipLaunchKernelGGL(series_combine_kernel, dim3(batch), dim3(256), 0, s, partials, ct, n_terms, batch, nchunk, out);
-  INF_CHECK_LAUNCH();
+  // the Hutchinson dots' fp64 chunk partials of every term in, one fp32 log-det per sample out
+  INF_PROF_LAUNCH(s, 720, 8.0 * batch * nchunk * n_terms + 4.0 * batch, series_combine_kernel, dim3(batch), dim3(256),
+                  0, s, partials, ct, n_terms, batch, nchunk, out);
   return INF_OK;
 }
 

@@ -364,8 +364,21 @@ def profile_end():
                  bytes=arr[i].bytes, peak_ms=arr[i].peak_ms) for i in range(min(n.value, 256))]
 
 
+# Profiled launches of the HBM-bound phases (pointwise.hip / glue.hip INF_PROF_LAUNCH): tag -> kernel name (the
+# rocprofv3 Kernel_Name without namespace, template arguments and signature)
+PHASE_TAGS = {
+    700: 'resid_bcast_kernel', 701: 'resid_bcast_fc_kernel', 702: 'broyden_start_fc_kernel', 703: 'axpy_step_kernel',
+    704: 'neg_kernel', 705: 'reduce_partials_kernel', 706: 'recomp_kernel',
+    710: 'broyden_p1', 711: 'broyden_p2', 712: 'broyden_p3', 713: 'broyden_p4', 714: 'br_sum_chunks',
+    715: 'broyden_small_d_kernel',
+    720: 'series_combine_kernel', 721: 'rademacher_kernel',
+}
+
+
 def tag_name(tag):
     """Human/rocprof-readable name of a kernel tag (see gemm.hip run<> / pointwise.hip)."""
+    if tag in PHASE_TAGS:
+        return PHASE_TAGS[tag]
     if 500 <= tag < 540:     # 50x: net313_kernel (64-px tiles), 51x: _h (32-px, 2 per CU), 52x: _w (32-px, wide),
         #                      53x: net313k (128-px K-chunked VJP, fused313k.hip)
         return 'net313%s<%s>' % (['_kernel', '_kernel_h', '_kernel_w', 'k_kernel'][(tag - 500) // 10],
