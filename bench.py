@@ -311,6 +311,7 @@ def main():
     model = build_flow(arch, B)
     model.load_state_dict(sd, strict=True)
     model = model.to(device).eval()
+    dd.check_replicas(model, device)            # every rank builds its own copy: they must agree
     nsteps = args.warmup + args.steps
     if image:
         xs = torch.stack([syn.image_batch(B, arch['input_size'], arch['nvals'], seed=1000 * rank + i)

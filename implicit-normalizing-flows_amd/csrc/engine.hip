@@ -1559,9 +1559,10 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
     // than silently selecting another rule
     struct EnvOpt { const char* name; int* slot; const char* const* values; int n; };
     static const char* const k128_v[] = {"0", "1", "2"};
+    static const char* const k128_v4[] = {"0", "1", "2", "3"};
     static const char* const bin_v[] = {"0", "1"};
     static const char* const conv_v[] = {"global", "per_sample"};
-    const EnvOpt opts[] = {{"INFLOW_FUSED_K128", &n->k128, k128_v, 3},
+    const EnvOpt opts[] = {{"INFLOW_FUSED_K128", &n->k128, k128_v4, 4},
                            {"INFLOW_EVAL_OVERLAP", &n->eval_overlap, bin_v, 2},
                            {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2},
                            {"INFLOW_FC_BLOCK", &n->fc_block, k128_v, 3},
@@ -2685,7 +2686,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
   int* slot = nullptr;
   int lo = 0, hi = 0;
   switch (option) {
-    case INF_OPT_FUSED_K128: slot = &n->k128; hi = 2; break;
+    case INF_OPT_FUSED_K128: slot = &n->k128; hi = 3; break;
     case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
     case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;

@@ -302,8 +302,11 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
   }
 }
 
+#ifndef FC_FWD_NCB
+#define FC_FWD_NCB 3
+#endif
 int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
-  const int S = jac ? 16 : 48;
+  const int S = jac ? 16 : 16 * FC_FWD_NCB;
   const unsigned nb = (unsigned)((a.B + S - 1) / S);
 #define FCH(NCB_, JAC_, DD_)                                                                                     \
   do {                                                                                                           \
@@ -312,10 +315,10 @@ int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
     else hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SWISH, DD_>), dim3(nb), dim3(H3_NT), 0, s, a);      \
   } while (0)
   if (!jac) {
-    if (a.d == 6) FCH(3, false, 6);
-    else if (a.d == 2) FCH(3, false, 2);
-    else if (a.d == 8) FCH(3, false, 8);
-    else FCH(3, false, 0);
+    if (a.d == 6) FCH(FC_FWD_NCB, false, 6);
+    else if (a.d == 2) FCH(FC_FWD_NCB, false, 2);
+    else if (a.d == 8) FCH(FC_FWD_NCB, false, 8);
+    else FCH(FC_FWD_NCB, false, 0);
   } else if (a.d == 2) {
     FCH(3, true, 0);
   } else {

@@ -1127,7 +1127,10 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const int k128_pol = a0.k128;
   const bool k128 = k128_pol && H3_AC && h3_args && var == V64 && net313k_fits(hid, a0.C, a0.H, a0.W) &&
                     (k128_pol == 2 || (long)nnets * a0.B * (P / 128) >= 256);
-  const int tbn = k128 ? 128 : bn;
+  // the two-per-CU 64-pixel VJP (fused313p.hip): INF_OPT_FUSED_K128 = 3, VJP launches
+  const bool p64 = mode == MODE_VJP && k128_pol == 3 && H3_AC && h3_args && var == V64 &&
+                   net313p_fits(hid, a0.C, a0.H, a0.W);
+  const int tbn = p64 ? 64 : (k128 ? 128 : bn);
   for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < tbn ? a0.W : tbn;
   pr.nb0 = a0.B * (P / tbn);
   pr.max_ksplit = 8;
@@ -1140,7 +1143,17 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   const bool h3 = split && pr.a[0].A1h != nullptr && pr.a[1].A1h != nullptr;
   const bool prof = prof_enabled();
   if (prof) prof_begin_launch(s);
-  if (k128) {
+  if (p64) {
+    INF_TRY(launch_net313p(pr, nb, s));
+    if (prof) {
+      const double npx = (double)nnets * a0.B * P;
+      const double f = 2.0 * hid * 9.0 * a0.C + 2.0 * hid * hid + 2.0 * 9.0 * a0.C * hid;
+      const double bytes = 4.0 * npx * (a0.C + 2.0 * hid + 9.0 * a0.C);
+      prof_end_launch(s, 540 + mode, npx * f, bytes, npx * 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+    }
+    return INF_OK;
+  }
+  if (k128 && !p64) {
     INF_TRY(launch_net313k(pr, mode, nb, s));
     if (pr.tbuf) {
       char key[64];

@@ -206,6 +206,9 @@ int net313_supported(int hid, int C, int H, int W);
 // 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
 int net313k_fits(int hid, int C, int H, int W);
 int launch_net313k(const Net313Pair& pr, int mode, unsigned nb, hipStream_t s);
+// two-per-CU 64-pixel VJP (fused313p.hip, INF_MFMA_F16X3, MODE_VJP)
+int net313p_fits(int hid, int C, int H, int W);
+int launch_net313p(const Net313Pair& pr, unsigned nb, hipStream_t s);
 int launch_net313(const Net313Args& a, int hid, int mode, hipStream_t s);
 // layout_nets (> 0) picks the tile variant as if that many nets shared the grid: launches that write
 // derivatives for a paired series must use the pair's variant (the d1/d2 layout depends on it)

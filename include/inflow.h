@@ -119,7 +119,8 @@ int inf_net_get_mfma(const InfNet* net);
  *   INF_OPT_FUSED_K128    which kernel runs the fused VJP, forward (EVAL) and derivative-saving forwards (SAVE,
  *                         EVALSAVE) of 512-wide nets in INF_MFMA_F16X3:
  *                         0 the 64-pixel kernel only; 1 the 128-pixel K-chunked kernel where its grid still covers
- *                         all 256 CUs (default, or INFLOW_FUSED_K128 at inf_net_create); 2 wherever its tile fits.
+ *                         all 256 CUs (default, or INFLOW_FUSED_K128 at inf_net_create); 2 wherever its tile fits;
+ *                         3 as 1, with the VJP launches on the two-per-CU 64-pixel kernel (fused313p.hip).
  *                         A paired launch (both branches of an imBlock) follows the first net's value.
  *   INF_OPT_EVAL_OVERLAP  read on net_x of inf_imblock_eval: 1 (default; INFLOW_EVAL_OVERLAP=0 at create for 0) runs
  *                         the x-branch series on a side stream beside the root solve and the z-branch series (the
@@ -147,7 +148,7 @@ int inf_net_get_mfma(const InfNet* net);
  *                         layers or d = 2 with 1) as one launch for both nets: one forward pass keeping act' in registers,
  *                         then every term's VJP through the transposed weights' planes, dotted with the probe in the same
  *                         launch; 0 runs one GEMM launch per layer and term.
- * Unknown values of INFLOW_FUSED_K128 / INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP / INFLOW_FC_SERIES (0/1) and INFLOW_CONVERGENCE (global/per_sample)
+ * Unknown values of INFLOW_FUSED_K128 (0-3), INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP / INFLOW_FC_SERIES (0/1) and INFLOW_CONVERGENCE (global/per_sample)
  * make inf_net_create fail with INF_ERR_INVALID.
  * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
  * runs the VJP as autograd, implicit_block.py:418-426, and the two series one after the other, :300-322); results

@@ -60,3 +60,34 @@ def test_shards_partition_the_batch():
 def test_bits_per_dim_formula():
     # -mean(logpx) / ndim / ln 2  (train_img.py:549)
     assert abs(dd.bits_per_dim(-2 * 3072 * math.log(2) * 8.0, 2, 3072) - 8.0) < 1e-12
+
+
+def _replica_worker(rank, world, port, perturb, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from lib import synthetic as syn
+    from lib.configs import build_flow
+    arch = syn.TOY
+    m = build_flow(arch, 4)
+    m.load_state_dict(syn.make_state_dict(arch, 0), strict=True)
+    if perturb and rank == 1:
+        with torch.no_grad():
+            p = dict(m.named_parameters())['chain.2.nnet_z.2.weight']
+            p[3, 5] += 1e-6
+    try:
+        dd.check_replicas(m, 'cpu')
+        out[rank] = 0
+    except RuntimeError as e:
+        out[rank] = 1 if 'chain.2.nnet_z.2.weight' in str(e) else 2
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('perturb', [False, True])
+def test_replica_check_catches_divergent_weights(perturb):
+    """bench.py's start-up check (lib.distributed.check_replicas): every rank builds its own model, and one changed
+    weight on one rank makes every rank raise, naming the entry (gloo, 2 ranks)."""
+    world = 2
+    out = torch.zeros(world, dtype=torch.int64).share_memory_()
+    mp.spawn(_replica_worker, args=(world, _free_port(), perturb, out), nprocs=world, join=True)
+    assert out.tolist() == ([1, 1] if perturb else [0, 0])

@@ -553,7 +553,9 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew, exact_scale):
     skew: hidden units 256-511 of both hidden layers weighted 1000x (first conv's output rows, last conv's input
     channels), so the second 256-row chunk's column maxima far exceed the first's and the 128-pixel kernel's chunk 1
     leaves its fast put at chunk 0's scales for the exact-scale path.
-    exact_scale: INF_OPT_K128_EXACT_SCALE = 1 sends every tile through that path."""
+    exact_scale: INF_OPT_K128_EXACT_SCALE = 1 sends every tile through that path.
+    INF_OPT_FUSED_K128 = 3 runs the VJP launches on the two-per-CU 64-pixel kernel (fused313p.hip, same chunked
+    arithmetic and chunk-1 scale rules), checked against the same 64-pixel reference."""
     arch = syn.CIFAR10
     m, _ = _model(arch, B)
     blk = imblocks(m)[block]
@@ -584,9 +586,9 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew, exact_scale):
     k_prev = net.get_option(_hip.INF_OPT_FUSED_K128)
     assert net.set_option(_hip.INF_OPT_K128_EXACT_SCALE, exact_scale) == 0
     try:
-        for pol in (2, 0):
+        for pol in (2, 3, 0):
             prev = net.set_option(_hip.INF_OPT_FUSED_K128, pol)
-            assert prev in (0, 1, 2)
+            assert prev in (0, 1, 2, 3)
             y, g, ld, w = torch.empty_like(x), torch.empty_like(x), torch.empty(B, device=DEV), torch.empty_like(x)
             poison()
             _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(),
@@ -605,12 +607,13 @@ def test_fused_k128_vjp_matches_64px_kernel(block, B, skew, exact_scale):
     finally:
         net.set_option(_hip.INF_OPT_FUSED_K128, k_prev)
         net.set_option(_hip.INF_OPT_K128_EXACT_SCALE, 0)
-    assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_K128, 3) < 0
+    assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_K128, 4) < 0
     assert net.get_option(_hip.INF_OPT_FUSED_K128) == k_prev
-    for a in outs[2]:
-        assert torch.isfinite(a).all()
-    for a, b in zip(outs[2], outs[0]):
-        _close(a, b, rel=1e-5)
+    for pol in (2, 3):          # the 128-pixel kernel; the two-per-CU 64-pixel VJP (fused313p.hip)
+        for a in outs[pol]:
+            assert torch.isfinite(a).all()
+        for a, b in zip(outs[pol], outs[0]):
+            _close(a, b, rel=1e-5)
 
 
 def test_eval_overlap_matches_sequential():
