@@ -48,6 +48,8 @@ def _eval(m, x, fc_block, convergence):
         b.convergence = convergence
     loss, logpx, z = tabular_logpx(m, x)      # builds the engine nets on first use
     _set_block(m, fc_block)
+    if fc_block == 0:
+        monkeypatch.setattr(imb, '_chain_eligible', lambda n: True)
     _hip.profile_begin(20000)
     try:
         loss, logpx, z = tabular_logpx(m, x)
@@ -276,11 +278,14 @@ def test_fc_f16x3_error_at_fp32_level(arch):
     assert err['block'][0] <= 2.0 * err[0][1] + 2e-7, err
 
 
+@pytest.mark.parametrize('fc_block', [2, 0])
 @pytest.mark.parametrize('convergence', ['global', 'per_sample'])
-def test_chain_call_matches_block_by_block(convergence, monkeypatch):
+def test_chain_call_matches_block_by_block(convergence, fc_block, monkeypatch):
     """SequentialFlow of fc imBlocks in eval as one engine call (inf_flow_eval_exact_chain: the blocks back to back on
     the stream, the log-density steps on the device) against the blocks called one by one from Python: bitwise the same
-    z and log p, the same Broyden statistics per block."""
+    z and log p, the same Broyden statistics per block.  fc_block 2: every block on the block kernel (where the module
+    takes the chain); 0: the launch-per-iteration path, the chain forced (the module does not take it there: no gain,
+    DESIGN.md §11)."""
     import lib.layers.imblock as imb
     arch = syn.POWER
     B = 1000
@@ -289,7 +294,9 @@ def test_chain_call_matches_block_by_block(convergence, monkeypatch):
     for b in imblocks(m):
         b.convergence = convergence
     tabular_logpx(m, x)
-    _set_block(m, 2)                     # the chain runs where the blocks are block-kernel launches
+    _set_block(m, fc_block)
+    if fc_block == 0:
+        monkeypatch.setattr(imb, '_chain_eligible', lambda n: True)
     calls = []
     real = imb.eval_exact_chain
 
