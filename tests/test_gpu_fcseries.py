@@ -65,8 +65,13 @@ def _coeffs(n):
                     dtype=np.float32)
 
 
+POWER_SWISH = dict(syn.POWER, act='swish', n_blocks=2)      # the Swish instantiation (learned beta per layer)
+TOY_SWISH = dict(syn.TOY, act='swish', n_blocks=2)
+
+
 @pytest.mark.parametrize('arch,block,B,n', [(syn.POWER, 0, 257, 6), (syn.POWER, 7, 10000, 12), (syn.POWER, 19, 1, 1),
-                                            (syn.POWER, 3, 100, 100), (syn.TOY, 3, 130, 9), (syn.TOY, 0, 47, 30)])
+                                            (syn.POWER, 3, 100, 100), (syn.TOY, 3, 130, 9), (syn.TOY, 0, 47, 30),
+                                            (POWER_SWISH, 1, 300, 8), (TOY_SWISH, 0, 97, 5)])
 def test_fcseries_matches_oracle(arch, block, B, n):
     m, sd = _model(arch, B)
     blk = imblocks(m)[block]
