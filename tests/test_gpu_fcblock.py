@@ -48,8 +48,6 @@ def _eval(m, x, fc_block, convergence):
         b.convergence = convergence
     loss, logpx, z = tabular_logpx(m, x)      # builds the engine nets on first use
     _set_block(m, fc_block)
-    if fc_block == 0:
-        monkeypatch.setattr(imb, '_chain_eligible', lambda n: True)
     _hip.profile_begin(20000)
     try:
         loss, logpx, z = tabular_logpx(m, x)
