@@ -53,6 +53,7 @@ METRIC = {   # BASELINE.json metric for the CIFAR10 workload; the other configs 
     'cifar10_small': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CIFAR10 (idim 64) density eval',
     'celebahq256': 'samples/sec (whole node) + bits/dim \u0394 vs ref, CelebA-HQ 256 density eval',
     'power': 'samples/sec (whole node) + nats \u0394 vs ref, POWER tabular density eval',
+    'toy': 'samples/sec (whole node) + nats \u0394 vs ref, 2-D checkerboard toy density eval',
 }
 # --config -> (lib/synthetic.py architecture, per-GPU batch, global batch): BASELINE.json configs[1..4]
 BENCH_CONFIGS = {
@@ -61,6 +62,7 @@ BENCH_CONFIGS = {
     'cifar10_small': ('cifar10_small', 64, None),
     'celebahq256': ('celebahq256', 4, None),   # C5
     'power': ('power', 10000, None),           # C2
+    'toy': ('toy', 5000, None),                # C1 (the reference's CPU-runnable case; a GPU line here)
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 matrix peak (= f32 vector peak)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA peak (1024 flop/clk/SIMD x 1024 SIMDs x 2.4 GHz)
@@ -439,9 +441,14 @@ def main():
     peak = dom['flops'] / (dom['peak_ms'] * 1e9) if dom.get('peak_ms') else FP32_MFMA_PEAK_TFLOPS
     what = {'eval': 'density eval', 'train': 'training step',
             'trainfwd': 'train-mode forward (power-series log-det, no gradients)'}[args.mode]
+    ld_text = ('power-series log-det, Geometric(0.5) + 2 terms' if args.mode == 'trainfwd' else
+               'exact %dx%d log-det' % (arch['d'], arch['d']))
     if args.config == 'power':
         workload = ('power: POWER tabular implicit flow %s (run_tabular.sh arch: 20 imBlocks, 6-128x4-6 sin, '
-                    'coeff 0.99, exact 6x6 log-det), batch %d per GPU' % (what, B))
+                    'coeff 0.99, %s), batch %d per GPU' % (what, ld_text, B))
+    elif args.config == 'toy':
+        workload = ('toy: 2-D checkerboard implicit flow %s (run_toy.sh arch: 6 imBlocks, 2-128-128-2 sin, coeff 0.99, '
+                    '%s), batch %d per GPU' % (what, ld_text, B))
     elif global_batch is not None:
         workload = ('%s: CIFAR10 implicit flow %s (run_cifar10.sh arch), global batch %d sharded over %d GPU%s '
                     '(%d per GPU)' % (args.config, what, global_batch, world, 's' if world > 1 else '', B))
