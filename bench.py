@@ -207,6 +207,25 @@ def hbm_phases(stats, config, batch):
     return out
 
 
+def workload_text(args, arch, B, global_batch, world):
+    """config.workload of the bench line: the workload, the mode and the batch."""
+    what = {'eval': 'density eval', 'train': 'training step',
+            'trainfwd': 'train-mode forward (power-series log-det, no gradients)'}[args.mode]
+    if arch['kind'] != 'conv':
+        ld_text = ('power-series log-det, Geometric(0.5) + 2 terms' if args.mode == 'trainfwd' else
+                   'exact %dx%d log-det' % (arch['d'], arch['d']))
+        if args.config == 'power':
+            return ('power: POWER tabular implicit flow %s (run_tabular.sh arch: 20 imBlocks, 6-128x4-6 sin, '
+                    'coeff 0.99, %s), batch %d per GPU' % (what, ld_text, B))
+        return ('%s: 2-D checkerboard implicit flow %s (run_toy.sh arch: 6 imBlocks, 2-128-128-2 sin, coeff 0.99, '
+                '%s), batch %d per GPU' % (args.config, what, ld_text, B))
+    if global_batch is not None:
+        return ('%s: CIFAR10 implicit flow %s (run_cifar10.sh arch), global batch %d sharded over %d GPU%s '
+                '(%d per GPU)' % (args.config, what, global_batch, world, 's' if world > 1 else '', B))
+    return '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU' % (
+        args.config, what, '' if args.config == 'cifar10' else ' variant', B)
+
+
 def host_threads():
     """`nproc` of the host (BASELINE.md:36: the CPU baseline runs on N = nproc threads).  GNU nproc honours the
     process's CPU affinity and OMP_NUM_THREADS, i.e. the CPU share the job actually has; os.cpu_count() is the
@@ -439,22 +458,7 @@ def main():
     # fp32-equivalent peak of the arithmetic the dominant kernel issues: its algorithmic FLOPs over the time its
     # MFMA instructions take at their dense peak (engine prof peak_ms; frac = MFMA-pipe fraction)
     peak = dom['flops'] / (dom['peak_ms'] * 1e9) if dom.get('peak_ms') else FP32_MFMA_PEAK_TFLOPS
-    what = {'eval': 'density eval', 'train': 'training step',
-            'trainfwd': 'train-mode forward (power-series log-det, no gradients)'}[args.mode]
-    ld_text = ('power-series log-det, Geometric(0.5) + 2 terms' if args.mode == 'trainfwd' else
-               'exact %dx%d log-det' % (arch['d'], arch['d']))
-    if args.config == 'power':
-        workload = ('power: POWER tabular implicit flow %s (run_tabular.sh arch: 20 imBlocks, 6-128x4-6 sin, '
-                    'coeff 0.99, %s), batch %d per GPU' % (what, ld_text, B))
-    elif args.config == 'toy':
-        workload = ('toy: 2-D checkerboard implicit flow %s (run_toy.sh arch: 6 imBlocks, 2-128-128-2 sin, coeff 0.99, '
-                    '%s), batch %d per GPU' % (what, ld_text, B))
-    elif global_batch is not None:
-        workload = ('%s: CIFAR10 implicit flow %s (run_cifar10.sh arch), global batch %d sharded over %d GPU%s '
-                    '(%d per GPU)' % (args.config, what, global_batch, world, 's' if world > 1 else '', B))
-    else:
-        workload = '%s implicit flow %s (run_cifar10.sh arch%s), batch %d per GPU' % (
-            args.config, what, '' if args.config == 'cifar10' else ' variant', B)
+    workload = workload_text(args, arch, B, global_batch, world)
     out = {
         'metric': METRIC[args.config] if args.mode == 'eval' else
         ('samples/sec (whole node), %s train-mode forward (power-series log-det, no gradients)' % args.config)

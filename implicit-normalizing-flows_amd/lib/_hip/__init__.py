@@ -203,7 +203,10 @@ _ws = {}
 
 
 def workspace(device, nbytes):
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    """Scratch for an engine call on `device`, one buffer per (device, current stream): calls queued on one stream reuse
+    it in stream order; a call on another stream (another host thread, a user's side stream) gets its own."""
+    idx = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(int(nbytes * 1.1) + 4096, dtype=torch.uint8, device=device)

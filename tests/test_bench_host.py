@@ -68,3 +68,20 @@ def test_roofline_phases_from_profile_stats():
     assert ph['hutchinson']['kernels'][0]['kernel'] == 'series_combine_kernel'
     assert 'pmc_phases.json[cifar10_b64]' in ph['basis']
     assert bench.hbm_phases(stats, 'cifar10', 63)['basis'].endswith('no PMC record')
+
+
+@pytest.mark.parametrize('config', sorted(bench.BENCH_CONFIGS))
+@pytest.mark.parametrize('mode', ['eval', 'train', 'trainfwd'])
+def test_workload_text_of_every_config(config, mode):
+    """The bench line's config.workload for every --config / --mode (the text formatting runs after the timed region
+    on the GPU box, so a formatting error would lose the whole line)."""
+    from lib import synthetic as syn
+    arch_name, per_gpu, global_batch = bench.BENCH_CONFIGS[config]
+
+    class A:
+        pass
+    a = A()
+    a.config, a.mode = config, mode
+    text = bench.workload_text(a, syn.CONFIGS[arch_name], per_gpu or 8, global_batch, 1)
+    assert config.split('_')[0] in text and 'batch' in text
+    assert bench.METRIC[config]
