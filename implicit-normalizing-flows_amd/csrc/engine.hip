@@ -26,6 +26,16 @@
 #include "glue.h"
 #include "kernels.h"
 
+// Events the engine records between its own launches (the host's Broyden readbacks, the side-stream fork / join, the
+// profiling brackets) skip the system-scope fence: a system-scope release writes back and invalidates the caches, so the
+// next kernel starts with a cold L2 and the CP idles ≈ 5 µs per event (kernel trace).  What the host
+// reads through these events lives in coherent pinned memory written by the kernels / copies themselves.
+#ifndef INF_EV_SYSFENCE
+#define INF_EV_SYSFENCE 0
+#endif
+constexpr unsigned INF_EV_SYNC = hipEventDisableTiming | (INF_EV_SYSFENCE ? 0u : (unsigned)hipEventDisableSystemFence);
+constexpr unsigned INF_EV_TIMING = INF_EV_SYSFENCE ? 0u : (unsigned)hipEventDisableSystemFence;
+
 namespace inf {
 static thread_local int g_last_hip = 0;
 void set_hip_error(hipError_t e) { g_last_hip = (int)e; }
@@ -465,7 +475,7 @@ static int sums_slot(int i, int B, SumsSlot** out) {
       return INF_ERR_HIP;
     sl.cap = cap;
   }
-  if (!sl.ev && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) return INF_ERR_HIP;
+  if (!sl.ev && hipEventCreateWithFlags(&sl.ev, INF_EV_SYNC) != hipSuccess) return INF_ERR_HIP;
   *out = &sl;
   return INF_OK;
 }
@@ -1099,7 +1109,7 @@ int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logde
     if (g_bk_host) (void)hipHostFree(g_bk_host);
     g_bk_host = nullptr;
     g_bk_host_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&g_bk_host), nbytes + 16, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(reinterpret_cast<void**>(&g_bk_host), nbytes + 16, hipHostMallocCoherent) != hipSuccess)
       return INF_ERR_HIP;
     g_bk_host_cap = nbytes + 16;
   }
@@ -1108,7 +1118,7 @@ int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logde
   hipEvent_t ev = nullptr;
   {
     static thread_local hipEvent_t bk_ev = nullptr;
-    if (!bk_ev && hipEventCreateWithFlags(&bk_ev, hipEventDisableTiming) != hipSuccess) return INF_ERR_HIP;
+    if (!bk_ev && hipEventCreateWithFlags(&bk_ev, INF_EV_SYNC) != hipSuccess) return INF_ERR_HIP;
     ev = bk_ev;
   }
   INF_HIP(hipEventRecord(ev, s));
@@ -1940,8 +1950,8 @@ static SideStream* side_stream() {
   SideStream& ss = per_dev[dev];
   if (!ss.s) {
     if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&ss.fork, INF_EV_SYNC) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.join, INF_EV_SYNC) != hipSuccess)
       return nullptr;
   }
   return &ss;
@@ -2490,8 +2500,8 @@ int inf_profile_begin(int max_launches) {
   }
   g_prof.assign((size_t)max_launches, ProfSlot{});
   for (auto& p : g_prof) {
-    INF_HIP(hipEventCreate(&p.a));
-    INF_HIP(hipEventCreate(&p.b));
+    INF_HIP(hipEventCreateWithFlags(&p.a, INF_EV_TIMING));
+    INF_HIP(hipEventCreateWithFlags(&p.b, INF_EV_TIMING));
   }
   g_prof_used = 0;
   g_prof_on = true;
