@@ -2058,22 +2058,35 @@ int inf_imblock_eval(InfNet* nx, InfNet* nz, const float* x, float* z, const flo
   return series_fused(nets, xs, es, 2, coeff, n_terms, outs, B, bfs, s, /*save_mask=*/2u);
 }
 
-int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B,
-                           int T, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
-  if (!nx || !nz || !x || !z || !logdet_x || !logdet_z || B <= 0 || T <= 0 || T > 64 || !same_shape(nx, nz))
-    return INF_ERR_INVALID;
-  if (!nx->fcfused || !nz->fcfused || nx->d > 10) return INF_ERR_UNSUPPORTED;
-  {
-    FcArgs probe = fc_args(nx, x, B);
-    FcArgs probe_z = fc_args(nz, x, B);
-    if (!fcnet_supported(probe, true) || !fcnet_supported(probe_z, true)) return INF_ERR_UNSUPPORTED;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  Bufs bf;
-  if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+// The next block's x-branch folded into this block's z-branch Jacobian launch (the chain call): both evaluate their net
+// at this block's z, so one grid holds the two (launch_fcnet_jac_pair: 2 x 625 workgroups at B = 10 000 take 85 us
+// against 2 x 56 us as two launches).  bf: the next block's buffers (its xin / fx / xemb), logdet: its
+// logdet_x; done: the last launch this block queued was the pair (else the next block runs its own x-branch launch).
+struct FcNextX {
+  InfNet* nx = nullptr;
+  Bufs* bf = nullptr;
+  float* logdet = nullptr;
+  bool done = false;
+};
+// whether inf_imblock_eval_exact takes the block kernel (fcblock.hip) for this solved net
+static bool fc_block_first(const InfNet* nz) {
+  return nz->fc_block == 2 || (nz->fc_block == 1 && nz->convergence == INF_CONV_PER_SAMPLE);
+}
+// f16x3 planes on both nets of a pair launch, same shape
+static bool fc_pair_ok(const InfNet* a, const InfNet* b) {
+  return a->fcfused && b->fcfused && a->mfma_mode == INF_MFMA_F16X3 && b->mfma_mode == INF_MFMA_F16X3 &&
+         same_shape(a, b) && !a->L.empty() && !b->L.empty() && a->L[0].act == b->L[0].act;
+}
+
+// inf_imblock_eval_exact on carved buffers.  x_done: bf's xin / fx / xemb and logdet_x hold this block's x-branch
+// already (the previous block's pair launch); next (nullable): fold the next block's x-branch into the z-branch launch.
+static int eval_exact_fc(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B,
+                         int T, double eps, InfBroydenStats* stats, Bufs& bf, hipStream_t s, bool x_done,
+                         FcNextX* next) {
+  if (next) next->done = false;
   // x in the internal layout: written by the x-branch JAC launch's staging (it reads x in the boundary layout)
   const float* xi = bf.xin;
-  if (nz->fc_block == 2 || (nz->fc_block == 1 && nz->convergence == INF_CONV_PER_SAMPLE)) {
+  if (fc_block_first(nz)) {
     // the whole block in one launch (fcblock.hip); falls through to the launch-per-iteration path below when the
     // configuration has no block kernel or (global rule) its grid cannot be co-resident.  The default (1) takes it for
     // the per-sample rule only: under the global rule the launch path is faster
@@ -2087,18 +2100,21 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   // z = (f_x(x) - f_z(z*)) + x   (implicit_block.py:74-80, 227)
   OutArgs a;
   memset(&a, 0, sizeof(a));
-  FcArgs fjx = fc_args(nx, nullptr, B);
-  fjx.x_bnd = x;
-  fjx.x_int = bf.xin;
-  fjx.logdet = logdet_x;
-  fjx.o.in0 = xi;
-  fjx.o.out0 = bf.fx;
-  fjx.o.out1 = bf.xemb;
-  INF_TRY(launch_fcnet(fjx, true, s));
+  if (!x_done) {
+    FcArgs fjx = fc_args(nx, nullptr, B);
+    fjx.x_bnd = x;
+    fjx.x_int = bf.xin;
+    fjx.logdet = logdet_x;
+    fjx.o.in0 = xi;
+    fjx.o.out0 = bf.fx;
+    fjx.o.out1 = bf.xemb;
+    INF_TRY(launch_fcnet(fjx, true, s));
+  }
   // z = (f_x(x) - f_z(z*)) + x computed in the staging of the log|det(I + J_fz(z))| launch, which also writes z in the
   // boundary layout (the recompute and transpose launches of the path below, in one).  The solve queues it on its
   // predicted last iterate before it reads that iterate's norm (SpecTail), so the GPU does not wait for the host's
-  // stop decision; if the solve's result is another iterate (or it breaks), it is queued again on the result.
+  // stop decision; if the solve's result is another iterate (or it breaks), it is queued again on the result.  With
+  // next, the same launch evaluates the next block's x-branch at that z (its input recomputed in its own staging).
   auto jac_z = [&](const float* flow) {
     FcArgs fjz = fc_args(nz, nullptr, B);
     fjz.logdet = logdet_z;
@@ -2106,6 +2122,19 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
     fjz.rc_fz = flow;
     fjz.rc_x = xi;
     fjz.rc_out = z;
+    if (next) {
+      FcArgs fjn = fc_args(next->nx, nullptr, B);
+      fjn.rc_fx = bf.fx;
+      fjn.rc_fz = flow;
+      fjn.rc_x = xi;
+      fjn.x_int = next->bf->xin;
+      fjn.logdet = next->logdet;
+      fjn.o.out0 = next->bf->fx;
+      fjn.o.out1 = next->bf->xemb;
+      const int st = launch_fcnet_jac_pair(fjz, fjn, s);
+      next->done = st == INF_OK;
+      if (st != INF_ERR_UNSUPPORTED) return st;
+    }
     return launch_fcnet(fjz, true, s);
   };
   SpecTail tail;
@@ -2117,6 +2146,7 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
     if (tail.x && tail.x == bf.lowest && tail.f == bf.flow) return INF_OK;   // the speculative launch has the result
     return jac_z(bf.flow);
   }
+  if (next) next->done = false;
   memset(&a, 0, sizeof(a));
   a.in0 = bf.fx;
   a.in1 = xi;
@@ -2129,19 +2159,40 @@ int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, flo
   return to_boundary(nx, bf.tmp, z, B, s);
 }
 
+static int eval_exact_check(InfNet* nx, InfNet* nz, const float* x, int B) {
+  if (!nx->fcfused || !nz->fcfused || nx->d > 10) return INF_ERR_UNSUPPORTED;
+  FcArgs probe = fc_args(nx, x, B);
+  FcArgs probe_z = fc_args(nz, x, B);
+  if (!fcnet_supported(probe, true) || !fcnet_supported(probe_z, true)) return INF_ERR_UNSUPPORTED;
+  return INF_OK;
+}
+
+int inf_imblock_eval_exact(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B,
+                           int T, double eps, InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
+  if (!nx || !nz || !x || !z || !logdet_x || !logdet_z || B <= 0 || T <= 0 || T > 64 || !same_shape(nx, nz))
+    return INF_ERR_INVALID;
+  INF_TRY(eval_exact_check(nx, nz, x, B));
+  Bufs bf;
+  if (!ws || carve(nz, B, T, ws, ws_bytes, bf) > ws_bytes) return INF_ERR_WORKSPACE;
+  return eval_exact_fc(nx, nz, x, z, logdet_x, logdet_z, B, T, eps, stats, bf, (hipStream_t)stream, false, nullptr);
+}
+
 size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int batch, const int* thresholds) {
   if (!net_z || n_blocks <= 0 || batch <= 0 || !thresholds) return 0;
   size_t blk = 0;
   for (int i = 0; i < n_blocks; ++i)
     if (net_z[i]) blk = std::max(blk, inf_workspace_bytes(net_z[i], batch, thresholds[i]));
   const size_t d = net_z[0] ? (size_t)net_z[0]->d : 0;
-  return blk + 256 * 4 + sizeof(float) * ((size_t)2 * batch * d + (size_t)4 * batch);
+  // two block workspaces (consecutive blocks alternate: the pair launch writes the next block's buffers while this
+  // block's are live), two z and logp buffers, two logdet_x / logdet_z pairs
+  return 2 * ((blk + 255) & ~(size_t)255) + 256 * 8 + sizeof(float) * ((size_t)2 * batch * d + (size_t)6 * batch);
 }
 
 // SequentialFlow of fc imBlocks in eval (train_tabular.py:314-336; container.py:12-20): block i is
 // inf_imblock_eval_exact on the previous block's z, its log-density step logp <- logp - (logdet_x - logdet_z) on the device
 // (implicit_block.py:234), the blocks back to back on the stream with no host round trip between them beyond the ones a
-// block itself makes.
+// block itself makes.  On the launch path (global rule, f16x3 nets) block i's z-branch Jacobian launch also evaluates
+// block i + 1's x-branch (FcNextX): consecutive blocks alternate between two workspaces and logdet buffers.
 int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_blocks, const float* x, float* z,
                               const float* logp_in, float* logp_out, int B, const int* thresholds, const double* eps,
                               InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
@@ -2151,15 +2202,16 @@ int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_
     InfNet *nx = net_x[i], *nz = net_z[i];
     if (!nx || !nz || !same_shape(nx, nz) || !same_shape(nz, net_z[0]) || thresholds[i] <= 0 || thresholds[i] > 64)
       return INF_ERR_INVALID;
-    if (!nx->fcfused || !nz->fcfused || nx->d > 10) return INF_ERR_UNSUPPORTED;
-    FcArgs px = fc_args(nx, x, B), pz = fc_args(nz, x, B);
-    if (!fcnet_supported(px, true) || !fcnet_supported(pz, true)) return INF_ERR_UNSUPPORTED;
+    INF_TRY(eval_exact_check(nx, nz, x, B));
   }
   if (!ws || ws_bytes < inf_flow_chain_workspace_bytes(net_z, n_blocks, B, thresholds)) return INF_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   const size_t E = (size_t)B * net_z[0]->d;
+  size_t blk = 0;
+  for (int i = 0; i < n_blocks; ++i) blk = std::max(blk, inf_workspace_bytes(net_z[i], B, thresholds[i]));
+  blk = (blk + 255) & ~(size_t)255;
   char* base = reinterpret_cast<char*>(ws);
-  size_t off = 0;
+  size_t off = 2 * blk;
   auto take = [&](size_t bytes) {
     off = (off + 255) & ~(size_t)255;
     char* p = base + off;
@@ -2167,21 +2219,37 @@ int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_
     return reinterpret_cast<float*>(p);
   };
   float* zb[2] = {take(sizeof(float) * E), take(sizeof(float) * E)};
-  float* ldx = take(sizeof(float) * B);
-  float* ldz = take(sizeof(float) * B);
+  float* ldx[2] = {take(sizeof(float) * B), take(sizeof(float) * B)};
+  float* ldz[2] = {take(sizeof(float) * B), take(sizeof(float) * B)};
   float* lp[2] = {take(sizeof(float) * B), take(sizeof(float) * B)};
-  off = (off + 255) & ~(size_t)255;
-  void* bws = base + off;
-  const size_t bws_bytes = ws_bytes - off;
+  Bufs bfs[2];
+  auto carve_block = [&](int i) {
+    return carve(net_z[i], B, thresholds[i], base + (size_t)(i & 1) * blk, blk, bfs[i & 1]) <= blk ? INF_OK
+                                                                                                   : INF_ERR_WORKSPACE;
+  };
+  INF_TRY(carve_block(0));
   const float* in = x;
   const float* lin = logp_in;
+  bool x_done = false;
   for (int i = 0; i < n_blocks; ++i) {
     const bool last = i == n_blocks - 1;
     float* out = last ? z : zb[i & 1];
     float* lout = last ? logp_out : lp[i & 1];
-    INF_TRY(inf_imblock_eval_exact(net_x[i], net_z[i], in, out, ldx, ldz, B, thresholds[i], eps[i],
-                                   stats ? &stats[i] : nullptr, bws, bws_bytes, stream));
-    INF_TRY(glue_logp_step(lin, ldx, ldz, lout, B, s));
+    FcNextX nxt;
+    FcNextX* np = nullptr;
+    if (!last) {
+      INF_TRY(carve_block(i + 1));
+      if (!fc_block_first(net_z[i]) && !fc_block_first(net_z[i + 1]) && fc_pair_ok(net_z[i], net_x[i + 1])) {
+        nxt.nx = net_x[i + 1];
+        nxt.bf = &bfs[(i + 1) & 1];
+        nxt.logdet = ldx[(i + 1) & 1];
+        np = &nxt;
+      }
+    }
+    INF_TRY(eval_exact_fc(net_x[i], net_z[i], in, out, ldx[i & 1], ldz[i & 1], B, thresholds[i], eps[i],
+                          stats ? &stats[i] : nullptr, bfs[i & 1], s, x_done, np));
+    INF_TRY(glue_logp_step(lin, ldx[i & 1], ldz[i & 1], lout, B, s));
+    x_done = np && nxt.done;
     in = out;
     lin = lout;
   }

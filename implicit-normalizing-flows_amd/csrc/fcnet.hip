@@ -345,4 +345,18 @@ int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s) {
   return INF_OK;
 }
 
+int launch_fcnet_jac_pair(const FcArgs& a0, const FcArgs& a1, hipStream_t s) {
+  if (!fcnet_supported(a0, true) || !fcnet_supported(a1, true)) return INF_ERR_UNSUPPORTED;
+  if (!a0.L[0].Ah || !a1.L[0].Ah || a0.d != a1.d || a0.act != a1.act) return INF_ERR_UNSUPPORTED;
+  const bool prof = prof_enabled();
+  if (prof) prof_begin_launch(s);
+  INF_TRY(launch_fcnet_h3_jac_pair(a0, a1, s));
+  if (prof) {
+    const double T = a0.d + 1;
+    const double f = (2.0 * a0.d * FC_H * 2 + (double)(a0.nl - 2) * 2.0 * FC_H * FC_H) * T * (a0.B + a1.B);
+    prof_end_launch(s, 602, f, 4.0 * (a0.B + a1.B) * a0.d * 2.0, 3.0 * f / PEAK_BF16_FLOPS_PER_MS);
+  }
+  return INF_OK;
+}
+
 }  // namespace inf

@@ -61,9 +61,9 @@ __device__ __forceinline__ void split4(const float (&v)[4], float S, uint2& h, u
 }
 }  // namespace
 
-// DD: the FWD kernels' d at compile time for the in-kernel Broyden update (0: runtime)
+// DD: the FWD kernels' d at compile time for the in-kernel Broyden update (0: runtime); bid: the workgroup's sample block
 template <int NCB, bool JAC, int ACT, int DD>
-__global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
+__device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
   constexpr int NC = 16 * NCB;
   constexpr int S = JAC ? 16 : NC;
   static_assert(NCB <= H3_NW, "one output column block per wave");
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
   const int B = a.B, d = a.d;
-  const long b0 = (long)blockIdx.x * S;
+  const long b0 = bid * S;
   const bool br_on = !JAC && a.br_on;
 
   // ---- input rows [0, 16) in fp32: x (primal), e_j (JAC tangent block j); br_on: rows [0, d) from the update below
@@ -93,7 +93,8 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
       } else if (JAC && a.rc_fx) {                     // z = (f_x(x) - f_z(z*)) + x, written out once per element
         const long e = (long)k * B + b;
         v = (a.rc_fx[e] - a.rc_fz[e]) + a.rc_x[e];
-        a.rc_out[b * d + k] = v;
+        if (a.rc_out) a.rc_out[b * d + k] = v;
+        if (a.x_int) a.x_int[e] = v;                   // (the pair launch's next-block x-branch: its internal input)
       } else {
         v = a.x[(long)k * B + b];
       }
@@ -287,7 +288,10 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
           const long ei = (long)i * B + b;
           const float v = fsum(i, tid) + bias[i];
           a.o.out0[ei] = v;
-          a.o.out1[ei] = v + (a.x_bnd ? a.x_bnd[b * DM + i] : a.o.in0[ei]);   // (x_int is this launch's output)
+          // (x_int is this launch's output: the input again from where the staging read it)
+          const float xin = a.x_bnd ? a.x_bnd[b * DM + i]
+                                    : (a.rc_fx ? (a.rc_fx[ei] - a.rc_fz[ei]) + a.rc_x[ei] : a.o.in0[ei]);
+          a.o.out1[ei] = v + xin;
         }
       }
       if (a.tang) {
@@ -300,6 +304,17 @@ __global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
       if (a.logdet) a.logdet[b] = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * 16 + tid); });
     }
   }
+}
+
+template <int NCB, bool JAC, int ACT, int DD>
+__global__ __launch_bounds__(H3_NT) void fcnet_h3_kernel(FcArgs a) {
+  fcnet_h3_body<NCB, JAC, ACT, DD>(a, blockIdx.x);
+}
+// two JAC launches of the same shape in one grid (launch_fcnet_jac_pair): workgroups [0, nb0) run p.a[0]
+template <int NCB, int ACT>
+__global__ __launch_bounds__(H3_NT) void fcnet_h3_pair_kernel(FcPair p) {
+  const int sel = (int)blockIdx.x >= p.nb0 ? 1 : 0;
+  fcnet_h3_body<NCB, true, ACT, 0>(p.a[sel], (long)blockIdx.x - (sel ? p.nb0 : 0));
 }
 
 #ifndef FC_FWD_NCB
@@ -325,6 +340,24 @@ int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
     FCH(7, true, 0);
   }
 #undef FCH
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
+int launch_fcnet_h3_jac_pair(const FcArgs& a0, const FcArgs& a1, hipStream_t s) {
+  FcPair p;
+  p.a[0] = a0;
+  p.a[1] = a1;
+  p.nb0 = (a0.B + 15) / 16;
+  const unsigned nb = (unsigned)(p.nb0 + (a1.B + 15) / 16);
+#define FCP(NCB_)                                                                                                \
+  do {                                                                                                           \
+    if (a0.act == ACT_SIN) hipLaunchKernelGGL((fcnet_h3_pair_kernel<NCB_, ACT_SIN>), dim3(nb), dim3(H3_NT), 0, s, p); \
+    else hipLaunchKernelGGL((fcnet_h3_pair_kernel<NCB_, ACT_SWISH>), dim3(nb), dim3(H3_NT), 0, s, p);          \
+  } while (0)
+  if (a0.d == 2) FCP(3);
+  else FCP(7);
+#undef FCP
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

@@ -252,8 +252,16 @@ struct FcArgs {
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);
+// two JAC launches in one grid (f16x3 nets of one shape and activation, e.g. block k's z-branch log-det and block k + 1's
+// x-branch log-det + x_embed at the same input): INF_ERR_UNSUPPORTED unless both have f16x3 planes and kernels
+struct FcPair {
+  FcArgs a[2];
+  int nb0;                // workgroups of a[0]
+};
+int launch_fcnet_jac_pair(const FcArgs& a0, const FcArgs& a1, hipStream_t s);
 // the f16x3 kernels (fcnet_h3.hip; launch_fcnet dispatches there when a.L[0].Ah is set)
 int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s);
+int launch_fcnet_h3_jac_pair(const FcArgs& a0, const FcArgs& a1, hipStream_t s);
 // fc weight planes for the f16x3 kernels: the packed (M rows used, Kpad) fp32 operand -> nrt x nks fragment tiles of
 // 16 rows x 32 k, two scaled fp16 planes each, *exp_out = h3_scale_exp(max |A|)
 int launch_fc_split_h3(const float* A, int M, int Kpad, int nrt, int nks, uint16_t* dst, int* exp_out, hipStream_t s);

@@ -388,6 +388,8 @@ def tag_name(tag):
                                  ['EVAL', 'SAVE', 'VJP', 'EVALSAVE'][tag % 10])
     if tag in (600, 601):    # fused fc net (fcnet.hip): forward + fc_out epilogue / forward-mode Jacobian + LU
         return 'fcnet_kernel<%s>' % ('FWD', 'JAC')[tag - 600]
+    if tag == 602:           # two fc JAC launches in one grid (block k's z-branch, block k + 1's x-branch)
+        return 'fcnet_kernel<JAC pair>'
     if tag == 610:           # one launch per fc imBlock evaluation (fcblock.hip)
         return 'fcblock_kernel'
     if tag == 620:           # the power series of an fc net pair in one launch (fcblock.hip)

@@ -37,6 +37,7 @@ __all__ = ['imBlock', 'set_probe_mode', 'set_probe_shard', 'set_convergence', 'R
 
 _PROBES = {'mode': 'reference', 'seed': 0, 'offset': 0, 'shard': None}
 _SOLVE = {'convergence': 'global'}
+_MFMA_F16X3 = 2           # include/inflow.h InfMfmaMode
 
 
 def set_probe_mode(mode, seed=0):
@@ -259,41 +260,51 @@ def _uninitialised_convs(net):
 
 class _ChainPlan:
     """The host-side state of inf_flow_eval_exact_chain for one (model, batch shape, device, convergence settings):
-    the native nets of every block, the ctypes argument arrays, the statistics buffers and the workspace.  Reused while
-    the engine tensors of every net keep their storage and version (a weight update re-runs the blocks' refresh)."""
+    the native nets of every block, the ctypes argument arrays and the workspace size.  Reused while the engine tensors
+    of every net keep their storage and version (a weight update re-runs the blocks' refresh).  The stream, workspace
+    and statistics buffers are per call (concurrent callers on other streams / threads share the plan)."""
 
     def __init__(self, blocks, x):
         lib = _hip.load()
         B, n = x.shape[0], len(blocks)
         self.B = B
         self.natives = [b._native(x) for b in blocks]
-        self.stream = self.natives[0][2]
         self.nx = (ctypes.c_void_p * n)(*[p[0].handle.value for p in self.natives])
         self.nz = (ctypes.c_void_p * n)(*[p[1].handle.value for p in self.natives])
         self.T = (ctypes.c_int * n)(*[int(b.threshold) for b in blocks])
         self.eps = (ctypes.c_double * n)(*[float(b.eps_forward) for b in blocks])
-        self.stats = (_hip.BroydenStats * n)()
-        self.samples = []
-        for i, p in enumerate(self.natives):
-            if p[1].get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE:
-                arrs = [(ctypes.c_int * B)() for _ in range(3)]
-                self.stats[i].sample_nstep, self.stats[i].sample_lowest_step, self.stats[i].sample_prot_break = [
-                    ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in arrs]
-                self.samples.append(arrs)
-            else:
-                self.samples.append(None)
-        self.ws = _hip.workspace(x.device, lib.inf_flow_chain_workspace_bytes(self.nz, n, B, self.T))
+        self.per_sample = [p[1].get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE
+                           for p in self.natives]
+        self.ws_bytes = lib.inf_flow_chain_workspace_bytes(self.nz, n, B, self.T)
         self.tensors = [t for p in self.natives for nn_ in p[:2] for t in nn_._tensors]
         self.sig = self.signature()
 
     def signature(self):
         return [(t.data_ptr(), t._version) for t in self.tensors]
 
+    def stats(self):
+        """Fresh statistics buffers for one call: the BroydenStats array and the per-sample arrays it points to."""
+        st = (_hip.BroydenStats * len(self.per_sample))()
+        samples = []
+        for i, ps in enumerate(self.per_sample):
+            if ps:
+                arrs = [(ctypes.c_int * self.B)() for _ in range(3)]
+                st[i].sample_nstep, st[i].sample_lowest_step, st[i].sample_prot_break = [
+                    ctypes.cast(a, ctypes.POINTER(ctypes.c_int)) for a in arrs]
+                samples.append(arrs)
+            else:
+                samples.append(None)
+        return st, samples
+
 
 def _chain_eligible(native_z):
-    """Whether the blocks run as block-kernel launches (INF_OPT_FC_BLOCK on the solved net), where the chain call pays."""
+    """Whether the chain call pays: the blocks run as block-kernel launches (INF_OPT_FC_BLOCK on the solved net), or
+    on the launch path with f16x3 nets, where each block's z-branch Jacobian launch also evaluates the next block's
+    x-branch (engine.hip FcNextX, one grid for the two)."""
     fcb = native_z.get_option(_hip.INF_OPT_FC_BLOCK)
-    return fcb == 2 or (fcb == 1 and native_z.get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE)
+    if fcb == 2 or (fcb == 1 and native_z.get_option(_hip.INF_OPT_CONVERGENCE) == _hip.INF_CONV_PER_SAMPLE):
+        return True
+    return native_z.lib.inf_net_get_mfma(native_z.handle) == _MFMA_F16X3
 
 
 def _chain_key(blocks, x):
@@ -317,10 +328,11 @@ def eval_exact_chain(blocks, x, logpx, owner=None):
     key = _chain_key(blocks, x)
     plan = owner.__dict__.get('_chain_plan') if owner is not None else None
     if plan is None or plan[0] != key:
-        # Only where the blocks run as block-kernel launches (INF_OPT_FC_BLOCK): there every block ends in a host
-        # readback, so the host work between blocks leaves the GPU idle, and one call removes it.  On the
-        # launch-per-iteration path a block returns with its z-branch Jacobian still queued, which hides part of the
-        # next block's host work (measured: tools/ab_chain.py).
+        # Where the blocks run as block-kernel launches (INF_OPT_FC_BLOCK) every block ends in a host readback, so
+        # the host work between blocks leaves the GPU idle, and one call removes it; on the launch path with f16x3
+        # nets the call folds each block's x-branch Jacobian into the previous block's z-branch launch.  Otherwise a
+        # block returns with its z-branch Jacobian still queued, which hides the next block's host work anyway
+        # (measured: tools/ab_chain.py).
         if not _chain_eligible(blocks[0]._native(x)[1]):
             return None
         plan = (key, _ChainPlan(blocks, x))
@@ -338,15 +350,17 @@ def eval_exact_chain(blocks, x, logpx, owner=None):
     z = torch.empty_like(x)
     lp_in = _logp_tensor(logpx, B, x.device)
     lp_out = torch.empty(B, device=x.device)
+    ws = _hip.workspace(x.device, p.ws_bytes)
+    stats, samples = p.stats()
     rc = lib.inf_flow_eval_exact_chain(p.nx, p.nz, n, _hip.ptr(x), _hip.ptr(z), _hip.ptr(lp_in), _hip.ptr(lp_out), B,
-                                       p.T, p.eps, p.stats, _hip.ptr(p.ws), p.ws.numel(), p.stream)
+                                       p.T, p.eps, stats, _hip.ptr(ws), ws.numel(), _hip.stream_of(x))
     if rc == _hip.INF_ERR_UNSUPPORTED:
         return None
     _hip.check(rc, 'inf_flow_eval_exact_chain')
     for i, b in enumerate(blocks):
-        d = p.stats[i].as_dict(int(b.threshold))
-        if p.samples[i] is not None:
-            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in p.samples[i]]
+        d = stats[i].as_dict(int(b.threshold))
+        if samples[i] is not None:
+            d['sample_nstep'], d['sample_lowest_step'], d['sample_prot_break'] = [list(a) for a in samples[i]]
         b.last_broyden = d
     return z, lp_out.view(B, 1)
 

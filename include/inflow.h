@@ -231,6 +231,8 @@ int inf_imblock_eval_exact(InfNet* net_x, InfNet* net_z, const float* x, float* 
  * inf_imblock_eval_exact on block i-1's z (block 0 on x) and the log-density step logp <- logp - (logdet_x - logdet_z)
  * on the device (implicit_block.py:234; logp_in NULL: 0), writing the last block's z and the final logp (batch).  No
  * host round trip between blocks beyond a block's own.  thresholds / eps: per block; stats: n_blocks entries or NULL.
+ * With f16x3 nets on the launch path, block i's z-branch log-det launch also evaluates block i+1's x-branch (log-det
+ * and x_embed at the same z): one grid for the two Jacobians; results identical to the blocks called one by one.
  * INF_ERR_UNSUPPORTED (before any launch) when a block is not on the fused fc path.
  * ws >= inf_flow_chain_workspace_bytes(net_z, n_blocks, batch, thresholds). */
 size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int batch, const int* thresholds);

@@ -281,9 +281,9 @@ def test_fc_f16x3_error_at_fp32_level(arch):
 def test_chain_call_matches_block_by_block(convergence, fc_block, monkeypatch):
     """SequentialFlow of fc imBlocks in eval as one engine call (inf_flow_eval_exact_chain: the blocks back to back on
     the stream, the log-density steps on the device) against the blocks called one by one from Python: bitwise the same
-    z and log p, the same Broyden statistics per block.  fc_block 2: every block on the block kernel (where the module
-    takes the chain); 0: the launch-per-iteration path, the chain forced (the module does not take it there: no gain,
-    DESIGN.md §11)."""
+    z and log p, the same Broyden statistics per block.  fc_block 2: every block on the block kernel; 0: the
+    launch-per-iteration path, where every block's z-branch Jacobian launch also evaluates the next block's x-branch
+    (one grid for the two, tag 602)."""
     import lib.layers.imblock as imb
     arch = syn.POWER
     B = 1000
@@ -293,8 +293,6 @@ def test_chain_call_matches_block_by_block(convergence, fc_block, monkeypatch):
         b.convergence = convergence
     tabular_logpx(m, x)
     _set_block(m, fc_block)
-    if fc_block == 0:
-        monkeypatch.setattr(imb, '_chain_eligible', lambda n: True)
     calls = []
     real = imb.eval_exact_chain
 
@@ -303,9 +301,21 @@ def test_chain_call_matches_block_by_block(convergence, fc_block, monkeypatch):
         calls.append(out is not None)
         return out
     monkeypatch.setattr(imb, 'eval_exact_chain', spy)
-    loss_c, lp_c, z_c = tabular_logpx(m, x)
+    _hip.profile_begin(20000)
+    try:
+        loss_c, lp_c, z_c = tabular_logpx(m, x)
+        torch.cuda.synchronize()
+    finally:
+        launches = {s_['tag']: s_['launches'] for s_ in _hip.profile_end()}
     st_c = [dict(b.last_broyden) for b in imblocks(m)]
     assert calls == [True]
+    nb = len(imblocks(m))
+    if fc_block == 0:
+        # block 0's x-branch and the last block's z-branch alone; every other Jacobian in a pair launch (once per block
+        # boundary, again only where the speculative one was queued on another iterate)
+        assert launches.get(602, 0) >= nb - 1 and launches.get(601, 0) >= 2, launches
+    else:
+        assert 602 not in launches, launches
     monkeypatch.setattr(imb, 'eval_exact_chain', lambda *a, **k: None)
     loss_b, lp_b, z_b = tabular_logpx(m, x)
     st_b = [dict(b.last_broyden) for b in imblocks(m)]
