@@ -71,58 +71,6 @@ __device__ __forceinline__ f32x4 mfma3(const u32x4 (&a)[2], const u32x4& xh, con
   return c;
 }
 
-// The hidden activations in short inline forms (the precise sinf / cosf expand to hundreds of instructions per call,
-// which put this kernel's code out of the instruction cache).  Sin (activations.py:7-12): sin(2 pi a) / (2 pi) and its
-// derivative cos(2 pi a).  The argument is in revolutions, so the reduction r = a - rint(a) is exact (|a| < 2^22);
-// one fold to |r| <= 1/4 (exact), then Taylor polynomials in x = 2 pi r, |x| <= pi/2, through x^13 / x^14
-// (truncation <= 7e-10): within a few ulp of the correctly rounded values.  Swish: common.h's fast forms.
-__device__ __forceinline__ void sincos_2pi(float a, float& sn, float& cs) {
-  const float r = a - __builtin_rintf(a);
-  const bool fold = fabsf(r) > 0.25f;
-  const float t = fold ? __builtin_copysignf(0.5f, r) - r : r;
-  const float x = t * TWO_PI_F, x2 = x * x;
-  float ps = -1.f / 6227020800.f;                // sin: x (1 - x^2/3! + ... - x^12/13!)
-  ps = __builtin_fmaf(ps, x2, 1.f / 39916800.f);
-  ps = __builtin_fmaf(ps, x2, -1.f / 362880.f);
-  ps = __builtin_fmaf(ps, x2, 1.f / 5040.f);
-  ps = __builtin_fmaf(ps, x2, -1.f / 120.f);
-  ps = __builtin_fmaf(ps, x2, 1.f / 6.f);
-  ps = __builtin_fmaf(-ps, x2, 1.f);
-  float pc = 1.f / 87178291200.f;                // cos: 1 - x^2/2! + ... + x^14/14!
-  pc = __builtin_fmaf(pc, x2, -1.f / 479001600.f);
-  pc = __builtin_fmaf(pc, x2, 1.f / 3628800.f);
-  pc = __builtin_fmaf(pc, x2, -1.f / 40320.f);
-  pc = __builtin_fmaf(pc, x2, 1.f / 720.f);
-  pc = __builtin_fmaf(pc, x2, -1.f / 24.f);
-  pc = __builtin_fmaf(pc, x2, 0.5f);
-  pc = __builtin_fmaf(-pc, x2, 1.f);
-  sn = x * ps;
-  cs = fold ? -pc : pc;
-}
-template <int ACT>
-__device__ __forceinline__ float bk_act_f(float a, float sp) {
-  if constexpr (ACT == ACT_SIN) {
-    float sn, cs;
-    sincos_2pi(a, sn, cs);
-    return sn * (0.5f / PI_F);
-  } else {
-    return swish_fast_f(a, sp);
-  }
-}
-// act and act' together (JAC)
-template <int ACT>
-__device__ __forceinline__ void bk_act_fd(float a, float sp, float& f, float& d) {
-  if constexpr (ACT == ACT_SIN) {
-    float sn, cs;
-    sincos_2pi(a, sn, cs);
-    f = sn * (0.5f / PI_F);
-    d = cs;
-  } else {
-    f = swish_fast_f(a, sp);
-    d = swish_fast_d(a, sp);
-  }
-}
-
 template <int NKS>
 __device__ __forceinline__ void ldw(const uint16_t* A, int nks, int rt, int lane, u32x4 (&w)[NKS][2]) {
   const u32x4* p = reinterpret_cast<const u32x4*>(A);
@@ -287,16 +235,16 @@ __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, cons
         for (int cb = 0; cb < NCB; ++cb) v[cb][r] *= D->d[NH - l][cb][r];
       } else if constexpr (SV == SV_SAVE) {
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) bk_act_fd<ACT>(v[cb][r] + bias[r], sp, v[cb][r], D->d[l][cb][r]);
+        for (int cb = 0; cb < NCB; ++cb) fc_act_fd<ACT>(v[cb][r] + bias[r], sp, v[cb][r], D->d[l][cb][r]);
       } else if constexpr (JAC) {
         const float z = v[0][r] + bias[r];
         float dd;
-        bk_act_fd<ACT>(z, sp, v[0][r], dd);
+        fc_act_fd<ACT>(z, sp, v[0][r], dd);
 #pragma unroll
         for (int cb = 1; cb < NCB; ++cb) v[cb][r] *= dd;
       } else {
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) v[cb][r] = bk_act_f<ACT>(v[cb][r] + bias[r], sp);
+        for (int cb = 0; cb < NCB; ++cb) v[cb][r] = fc_act_f<ACT>(v[cb][r] + bias[r], sp);
       }
     }
 #pragma unroll
@@ -442,7 +390,7 @@ __device__ __forceinline__ void mlp_jac2(const FcArgs& a, const Pass& P, Stamps*
       for (int r = 0; r < 4; ++r) {
         const float z = v[t][0][r] + L.b[16 * (2 * rg + t) + 4 * g + r];
         float dd;
-        bk_act_fd<ACT>(z, sp, v[t][0][r], dd);
+        fc_act_fd<ACT>(z, sp, v[t][0][r], dd);
 #pragma unroll
         for (int j = 1; j < NJ; ++j) v[t][j][r] *= dd;
       }

@@ -177,4 +177,57 @@ __device__ __forceinline__ float logdet_lu(F J) {
   return sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
 }
 
+// The hidden activations of the f16x3 fc kernels (fcnet_h3.hip, fcblock.hip) in short inline forms: the precise sinf /
+// cosf expand to hundreds of instructions per call (out of the block kernel's instruction cache, and most of the VALU
+// of the latency-bound FWD / JAC launches), the precise swish two IEEE divisions and a range-reduced expf.  Sin (activations.py:7-12): sin(2 pi a) / (2 pi) and its
+// derivative cos(2 pi a).  The argument is in revolutions, so the reduction r = a - rint(a) is exact (|a| < 2^22);
+// one fold to |r| <= 1/4 (exact), then Taylor polynomials in x = 2 pi r, |x| <= pi/2, through x^13 / x^14
+// (truncation <= 7e-10): within a few ulp of the correctly rounded values.  Swish: common.h's fast forms.
+__device__ __forceinline__ void sincos_2pi(float a, float& sn, float& cs) {
+  const float r = a - __builtin_rintf(a);
+  const bool fold = fabsf(r) > 0.25f;
+  const float t = fold ? __builtin_copysignf(0.5f, r) - r : r;
+  const float x = t * TWO_PI_F, x2 = x * x;
+  float ps = -1.f / 6227020800.f;                // sin: x (1 - x^2/3! + ... - x^12/13!)
+  ps = __builtin_fmaf(ps, x2, 1.f / 39916800.f);
+  ps = __builtin_fmaf(ps, x2, -1.f / 362880.f);
+  ps = __builtin_fmaf(ps, x2, 1.f / 5040.f);
+  ps = __builtin_fmaf(ps, x2, -1.f / 120.f);
+  ps = __builtin_fmaf(ps, x2, 1.f / 6.f);
+  ps = __builtin_fmaf(-ps, x2, 1.f);
+  float pc = 1.f / 87178291200.f;                // cos: 1 - x^2/2! + ... + x^14/14!
+  pc = __builtin_fmaf(pc, x2, -1.f / 479001600.f);
+  pc = __builtin_fmaf(pc, x2, 1.f / 3628800.f);
+  pc = __builtin_fmaf(pc, x2, -1.f / 40320.f);
+  pc = __builtin_fmaf(pc, x2, 1.f / 720.f);
+  pc = __builtin_fmaf(pc, x2, -1.f / 24.f);
+  pc = __builtin_fmaf(pc, x2, 0.5f);
+  pc = __builtin_fmaf(-pc, x2, 1.f);
+  sn = x * ps;
+  cs = fold ? -pc : pc;
+}
+template <int ACT>
+__device__ __forceinline__ float fc_act_f(float a, float sp) {
+  if constexpr (ACT == ACT_SIN) {
+    float sn, cs;
+    sincos_2pi(a, sn, cs);
+    return sn * (0.5f / PI_F);
+  } else {
+    return swish_fast_f(a, sp);
+  }
+}
+// act and act' together (JAC)
+template <int ACT>
+__device__ __forceinline__ void fc_act_fd(float a, float sp, float& f, float& d) {
+  if constexpr (ACT == ACT_SIN) {
+    float sn, cs;
+    sincos_2pi(a, sn, cs);
+    f = sn * (0.5f / PI_F);
+    d = cs;
+  } else {
+    f = swish_fast_f(a, sp);
+    d = swish_fast_d(a, sp);
+  }
+}
+
 }  // namespace inf

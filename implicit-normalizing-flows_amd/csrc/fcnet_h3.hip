@@ -169,14 +169,13 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if constexpr (JAC) {
-        const float z = v[0][r] + bias[r];
-        const float dd = act_d<ACT>(z, sp);
-        v[0][r] = act_f<ACT>(z, sp);
+        float dd;
+        fc_act_fd<ACT>(v[0][r] + bias[r], sp, v[0][r], dd);
 #pragma unroll
         for (int cb = 1; cb < NCB; ++cb) v[cb][r] *= dd;
       } else {
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) v[cb][r] = act_f<ACT>(v[cb][r] + bias[r], sp);
+        for (int cb = 0; cb < NCB; ++cb) v[cb][r] = fc_act_f<ACT>(v[cb][r] + bias[r], sp);
       }
     }
     // column maxima: the 4 rows of a lane, the 4 lane groups of a column (shuffles), the 8 waves (LDS)
