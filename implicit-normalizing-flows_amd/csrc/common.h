@@ -1,6 +1,7 @@
 // Shared device helpers and host error plumbing for libinflow (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 #include "../../include/inflow.h"

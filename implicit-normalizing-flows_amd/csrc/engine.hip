@@ -180,6 +180,10 @@ struct Bufs {
   size_t bk_sync_bytes;
   char* bk_out;
   size_t bk_out_bytes;
+  // fc root solve, global rule (broyden_core zero-copy readback): the slot's event, bound by the residual launch itself
+  // (OutArgs::stop_ev) when its launcher can, which sets stop_bound; enqueue_sumsq then records no marker after it
+  hipEvent_t stop_ev = nullptr;
+  bool stop_bound = false;
 };
 
 size_t per_sample_hidden(const InfNet* n) { return (size_t)n->hidden_max * (n->fc ? 1 : n->P); }
@@ -496,6 +500,10 @@ int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const
   const bool ps_on = ps && ps->on;
   const bool direct = f->fc && !ps_on;
   if (direct && bf.part == sl->host) {               // the residual launch wrote the sums into the slot itself
+    const bool bound = bf.stop_bound && bf.stop_ev == sl->ev;
+    bf.stop_bound = false;
+    if (bound) return INF_OK;                        // ... and its launch completes the event (no marker packet: the
+                                                     // marker after a launch idles the GPU ~4.4 us)
     INF_HIP(hipEventRecord(sl->ev, s));
     return INF_OK;
   }
@@ -570,6 +578,8 @@ int eval_resid_part(InfNet* f, const float* z, const float* zsub, const float* x
   a.out2 = bf.fcur;
   a.partial = bf.part;
   a.nchunk = bf.nchunk;
+  a.stop_ev = bf.stop_ev;
+  a.stop_bound = &bf.stop_bound;
   return run_forward(f, z, B, bf, OM_RESID, &a, s);
 }
 // the same, synchronously, with the per-sample sums of squares on the host
@@ -731,10 +741,18 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   struct PartRestore {
     Bufs& b;
     double* p;
-    ~PartRestore() { b.part = p; }
-  } part_restore{bf, bf.part};
+    hipEvent_t e;
+    ~PartRestore() {
+      b.part = p;
+      b.stop_ev = e;
+      b.stop_bound = false;
+    }
+  } part_restore{bf, bf.part, bf.stop_ev};
   auto target = [&](SumsSlot* sl) {
-    if (zc) bf.part = sl->host;
+    if (zc) {
+      bf.part = sl->host;
+      bf.stop_ev = sl->ev;
+    }
   };
   target(slot[0]);
   float* xp = nullptr;
@@ -1022,6 +1040,8 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     a.out2 = bf.fcur;
     a.partial = bf.part;
     a.nchunk = bf.nchunk;
+    a.stop_ev = bf.stop_ev;
+    a.stop_bound = &bf.stop_bound;
     a.mode = OM_RESID;
     a.bias = f->L.back().b;
     FcArgs fa = fc_args(f, ba.xnew, B);
@@ -1032,7 +1052,8 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   };
   const StartFn start = [&](float* x0, float* g0, float* upd, float* x1, float* dx) {
     first = false;
-    return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, upd, x1, dx, B, f->d, s);
+    return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, bf.stop_ev, &bf.stop_bound, upd, x1, dx,
+                                   B, f->d, s);
   };
   INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
                        f->fc ? &start : nullptr, tail));

@@ -328,6 +328,27 @@ int launch_fcnet_h3(const FcArgs& a, bool jac, hipStream_t s) {
       hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SIN, DD_>), dim3(nb), dim3(H3_NT), 0, s, a);           \
     else hipLaunchKernelGGL((fcnet_h3_kernel<NCB_, JAC_, ACT_SWISH, DD_>), dim3(nb), dim3(H3_NT), 0, s, a);      \
   } while (0)
+  // FWD whose readback event completes with the launch itself (OutArgs::stop_ev; not while profiling, whose events
+  // bracket every launch)
+  const bool bind = !jac && a.o.stop_ev && !prof_enabled();
+#define FCE(NCB_, DD_)                                                                                           \
+  do {                                                                                                           \
+    if (a.act == ACT_SIN)                                                                                        \
+      hipExtLaunchKernelGGL((fcnet_h3_kernel<NCB_, false, ACT_SIN, DD_>), dim3(nb), dim3(H3_NT), 0, s, nullptr,  \
+                            a.o.stop_ev, 0, a);                                                                  \
+    else hipExtLaunchKernelGGL((fcnet_h3_kernel<NCB_, false, ACT_SWISH, DD_>), dim3(nb), dim3(H3_NT), 0, s,      \
+                               nullptr, a.o.stop_ev, 0, a);                                                      \
+  } while (0)
+  if (bind) {
+    if (a.d == 6) FCE(FC_FWD_NCB, 6);
+    else if (a.d == 2) FCE(FC_FWD_NCB, 2);
+    else if (a.d == 8) FCE(FC_FWD_NCB, 8);
+    else FCE(FC_FWD_NCB, 0);
+    INF_CHECK_LAUNCH();
+    *a.o.stop_bound = true;
+    return INF_OK;
+  }
+#undef FCE
   if (!jac) {
     if (a.d == 6) FCH(FC_FWD_NCB, false, 6);
     else if (a.d == 2) FCH(FC_FWD_NCB, false, 2);

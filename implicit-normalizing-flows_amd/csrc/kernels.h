@@ -56,6 +56,10 @@ struct OutArgs {
   const float* pre_beta;  // OM_VJP: multiply by swish'(in1) (preact input derivative)
   double* partial;        // (B, nchunk) per-sample partial sums (OM_RESID: g^2, OM_VJP: v.eps)
   int nchunk;
+  // host side (not read by the kernels): an event for the launch itself to complete (hipExtLaunchKernel's stop event:
+  // no marker packet after it), and the flag the launcher sets when it bound it (fc readbacks, engine.hip enqueue_sumsq)
+  hipEvent_t stop_ev = nullptr;
+  bool* stop_bound = nullptr;
 };
 int out_nchunk(int per_sample);
 int launch_conv_out(const OutArgs& a, int batch, hipStream_t s);
@@ -134,7 +138,7 @@ int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, fl
                           int batch, int d, hipStream_t s);
 // x0 = 0, the residual at it, update = -g0, x1 = x0 + update, dx = x1 - x0 in one launch (fc layout)
 int launch_broyden_start_fc(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
-                            float* upd, float* x1, float* dx, int batch, int d, hipStream_t s);
+                            hipEvent_t stop_ev, bool* stop_bound, float* upd, float* x1, float* dx, int batch, int d, hipStream_t s);
 int launch_vjp_resid(const float* v, const float* y, const float* grad, const float* gprev, float* g, float* dg,
                      double* partial, int batch, int d, int nchunk, int fc, hipStream_t s);
 int launch_trace_series(const float* tang, const float* coeff, int n_terms, float* out, int d, int batch,

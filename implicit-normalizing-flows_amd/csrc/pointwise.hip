@@ -174,7 +174,15 @@ __global__ __launch_bounds__(256) void broyden_start_fc_kernel(const float* f0, 
   partial[b] = acc;
 }
 int launch_broyden_start_fc(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
-                            float* upd, float* x1, float* dx, int batch, int d, hipStream_t s) {
+                            hipEvent_t stop_ev, bool* stop_bound, float* upd, float* x1, float* dx, int batch, int d,
+                            hipStream_t s) {
+  if (stop_ev && !prof_enabled()) {            // the readback event completes with the launch itself
+    hipExtLaunchKernelGGL(broyden_start_fc_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, nullptr, stop_ev, 0, f0,
+                          xemb, x0, g, fcur, partial, upd, x1, dx, batch, d);
+    INF_CHECK_LAUNCH();
+    *stop_bound = true;
+    return INF_OK;
+  }
   INF_PROF_LAUNCH(s, 702, 28.0 * batch * d + 8.0 * batch, broyden_start_fc_kernel, dim3((batch + 255) / 256),
                   dim3(256), 0, s, f0, xemb, x0, g, fcur, partial, upd, x1, dx, batch, d);
   return INF_OK;

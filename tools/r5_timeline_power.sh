@@ -4,8 +4,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/tl_power
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/bench.py --config power --cpu-baseline 0 --steps 30 --warmup 3 > $O/bench.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/bench.py --config ${CFG:-power} --cpu-baseline 0 --steps 30 --warmup 3 > $O/bench.log 2>&1
 F=$(find $O/trace -name '*kernel_trace.csv' | head -1)
-python3 $R/tools/timeline_gaps.py $F --skip 0.3 > $O/gaps.txt
+python3 $R/tools/timeline_gaps.py $F --skip 0.3 --window 60 > $O/gaps.txt
 rm -rf $O/trace
-cat $O/gaps.txt | head -30
+tail -62 $O/gaps.txt

@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument('csv')
 ap.add_argument('--skip', type=float, default=0.4)
 ap.add_argument('--top', type=int, default=25)
+ap.add_argument('--window', type=int, default=0)
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.csv)))
 ks = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']) for r in rows)
@@ -53,3 +54,26 @@ for g, i in big:
     for j in range(max(0, i - 8), min(len(ks), i + 8)):
         s, e, n = ks[j]
         print('   %12.3f us  dur %9.3f us  %s' % ((s - ks[i][1]) / 1e3, (e - s) / 1e3, short(n)))
+
+# per kernel: launches, mean duration, and the idle gap before it, over the gaps shorter than 100 us (within a step)
+per = {}
+for j in range(1, len(ks)):
+    s, e, n = ks[j]
+    g = s - max(k[1] for k in ks[max(0, j - 4):j])
+    c = per.setdefault(short(n), [0, 0, 0, 0])
+    c[0] += 1
+    c[1] += e - s
+    if 0 < g < 1e5:
+        c[2] += g
+        c[3] += 1
+print('per kernel: launches, mean duration, total, mean idle gap before it (gaps < 100 us)')
+for n, (c, d, g, ng) in sorted(per.items(), key=lambda kv: -kv[1][1])[:a.top]:
+    print('  %6d  %9.2f us  %9.3f ms  gap %7.2f us  %s' % (c, d / c / 1e3, d / 1e6, g / max(ng, 1) / 1e3, n))
+
+# one window of consecutive kernels from the middle of the trace (a block's launch sequence)
+if a.window:
+    m = len(ks) // 2
+    print('--- %d kernels from the middle: start relative to the previous end, duration' % a.window)
+    for j in range(m, min(len(ks), m + a.window)):
+        s, e, n = ks[j]
+        print('   gap %9.2f us  dur %8.2f us  %s' % ((s - ks[j - 1][1]) / 1e3, (e - s) / 1e3, short(n)))
