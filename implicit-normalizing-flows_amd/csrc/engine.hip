@@ -2089,6 +2089,13 @@ struct FcNextX {
   float* logdet = nullptr;
   bool done = false;
 };
+// The block's log-density step lout = lin - (logdet_x - logdet_z) folded into its z-branch Jacobian launch (the chain
+// call); done: the last launch this block queued wrote it (else the caller runs glue_logp_step)
+struct FcLogpStep {
+  const float* lin = nullptr;
+  float* lout = nullptr;
+  bool done = false;
+};
 // whether inf_imblock_eval_exact takes the block kernel (fcblock.hip) for this solved net
 static bool fc_block_first(const InfNet* nz) {
   return nz->fc_block == 2 || (nz->fc_block == 1 && nz->convergence == INF_CONV_PER_SAMPLE);
@@ -2103,8 +2110,9 @@ static bool fc_pair_ok(const InfNet* a, const InfNet* b) {
 // already (the previous block's pair launch); next (nullable): fold the next block's x-branch into the z-branch launch.
 static int eval_exact_fc(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B,
                          int T, double eps, InfBroydenStats* stats, Bufs& bf, hipStream_t s, bool x_done,
-                         FcNextX* next) {
+                         FcNextX* next, FcLogpStep* lp = nullptr) {
   if (next) next->done = false;
+  if (lp) lp->done = false;
   // x in the internal layout: written by the x-branch JAC launch's staging (it reads x in the boundary layout)
   const float* xi = bf.xin;
   if (fc_block_first(nz)) {
@@ -2143,6 +2151,12 @@ static int eval_exact_fc(InfNet* nx, InfNet* nz, const float* x, float* z, float
     fjz.rc_fz = flow;
     fjz.rc_x = xi;
     fjz.rc_out = z;
+    if (lp) {
+      fjz.lp_in = lp->lin;
+      fjz.lp_ldx = logdet_x;
+      fjz.lp_out = lp->lout;
+      lp->done = true;
+    }
     if (next) {
       FcArgs fjn = fc_args(next->nx, nullptr, B);
       fjn.rc_fx = bf.fx;
@@ -2168,6 +2182,7 @@ static int eval_exact_fc(InfNet* nx, InfNet* nz, const float* x, float* z, float
     return jac_z(bf.flow);
   }
   if (next) next->done = false;
+  if (lp) lp->done = false;
   memset(&a, 0, sizeof(a));
   a.in0 = bf.fx;
   a.in1 = xi;
@@ -2267,9 +2282,12 @@ int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_
         np = &nxt;
       }
     }
+    FcLogpStep lps;
+    lps.lin = lin;
+    lps.lout = lout;
     INF_TRY(eval_exact_fc(net_x[i], net_z[i], in, out, ldx[i & 1], ldz[i & 1], B, thresholds[i], eps[i],
-                          stats ? &stats[i] : nullptr, bfs[i & 1], s, x_done, np));
-    INF_TRY(glue_logp_step(lin, ldx[i & 1], ldz[i & 1], lout, B, s));
+                          stats ? &stats[i] : nullptr, bfs[i & 1], s, x_done, np, &lps));
+    if (!lps.done) INF_TRY(glue_logp_step(lin, ldx[i & 1], ldz[i & 1], lout, B, s));
     x_done = np && nxt.done;
     in = out;
     lin = lout;

@@ -291,7 +291,11 @@ __global__ __launch_bounds__(64 * NW) void fcnet_kernel(FcArgs a) {
           for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * CW + tid);
         }
       }
-      if (a.logdet) a.logdet[b] = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * CW + tid); });
+      if (a.logdet) {
+        const float ld = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * CW + tid); });
+        a.logdet[b] = ld;
+        if (a.lp_out) a.lp_out[b] = (a.lp_in ? a.lp_in[b] : 0.f) - (a.lp_ldx[b] - ld);   // glue.hip logp_step_kernel
+      }
     }
   }
 }

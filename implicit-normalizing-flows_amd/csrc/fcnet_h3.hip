@@ -300,7 +300,11 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
           for (int j = 0; j < DM; ++j) a.tang[i * ld + (long)(j + 1) * B + b] = fsum(i, (j + 1) * 16 + tid);
         }
       }
-      if (a.logdet) a.logdet[b] = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * 16 + tid); });
+      if (a.logdet) {
+        const float ld = logdet_lu<DM>([&](int i, int j) { return fsum(i, (j + 1) * 16 + tid); });
+        a.logdet[b] = ld;
+        if (a.lp_out) a.lp_out[b] = (a.lp_in ? a.lp_in[b] : 0.f) - (a.lp_ldx[b] - ld);   // glue.hip logp_step_kernel
+      }
     }
   }
 }

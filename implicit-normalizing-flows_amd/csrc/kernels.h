@@ -253,6 +253,11 @@ struct FcArgs {
   // layout (d, B) (the transpose launch folded into the staging)
   const float* x_bnd;
   float* x_int;
+  // JAC with logdet and lp_out set (the z-branch log-det of a chained block): also the block's log-density step
+  // lp_out = lp_in - (lp_ldx - logdet) (glue.hip logp_step_kernel's expression; lp_in null: 0), implicit_block.py:234
+  const float* lp_in;
+  const float* lp_ldx;
+  float* lp_out;
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);

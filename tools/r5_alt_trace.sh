@@ -1,16 +1,15 @@
-# Kernel trace of the POWER bench with the in-tree library and with altlib/lib_$1.so (a timing variant built on the
-# CPU side); prints the per-kernel table of each (tools/timeline_gaps.py)
+# Kernel traces of the POWER bench (CFG to change the config) with the in-tree library and with each of
+# altlib/lib_<name>.so (timing variants built on the CPU side, tools/r5_build_alt.sh); the per-kernel table of each
 set -e
 R=$GRAFT_REPO_ROOT
 cd $R
 L=implicit-normalizing-flows_amd/lib/_hip/libinflow.so
-CFG=${CFG:-power} bash tools/r5_timeline_power.sh > /dev/null
-grep -A6 "per kernel" gpurun_out/tl_power/gaps.txt
-cp gpurun_out/tl_power/gaps.txt gpurun_out/tl_power/gaps_base.txt
 cp $L /tmp/libinflow_base.so
-cp altlib/lib_$1.so $L
-CFG=${CFG:-power} bash tools/r5_timeline_power.sh > /dev/null
-cp /tmp/libinflow_base.so $L
-echo "--- alt $1"
-grep -A6 "per kernel" gpurun_out/tl_power/gaps.txt
-cp gpurun_out/tl_power/gaps.txt gpurun_out/tl_power/gaps_$1.txt
+for v in base "$@"; do
+  if [ $v != base ]; then cp altlib/lib_$v.so $L; fi
+  CFG=${CFG:-power} bash tools/r5_timeline_power.sh > /dev/null
+  cp /tmp/libinflow_base.so $L
+  echo "--- $v"
+  grep -A5 "per kernel" gpurun_out/tl_power/gaps.txt
+  cp gpurun_out/tl_power/gaps.txt gpurun_out/tl_power/gaps_$v.txt
+done
