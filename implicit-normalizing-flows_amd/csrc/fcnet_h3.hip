@@ -67,7 +67,17 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
   constexpr int NC = 16 * NCB;
   constexpr int S = JAC ? 16 : NC;
   static_assert(NCB <= H3_NW, "one output column block per wave");
-  __shared__ __attribute__((aligned(16))) uint16_t pl[2][NC * H3_LD];   // activation planes h, l: [col][k]
+  // Sin nets: every hidden activation is in [-1 / (2 pi), 1 / (2 pi)], so one power-of-two scale 2^SFIX puts every
+  // value below 2^15 (no fp16 overflow) and the split keeps 22 bits of each value down to |v| ~ 2^-20 (below, the low
+  // piece is subnormal: an absolute error under 2^-41).  The FWD needs no column maxima then (their exchange across
+  // the waves was ~12 % of the launch), and with two plane buffers one barrier per layer.  The JAC primal column takes
+  // the same scale, so that it keeps the FWD kernel's bits (x_embed); its tangent columns are unbounded.
+  constexpr bool SIN = ACT == ACT_SIN;
+  constexpr bool FIXS = SIN && !JAC;
+  constexpr int SFIX = 17;
+  constexpr int NBUF = FIXS ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t pl[NBUF][2][NC * H3_LD];   // activation planes h, l: [col][k]
+  int cur = 0;                                                              // the buffer holding the layer input
   __shared__ __attribute__((aligned(16))) float tmp[16 * NC];           // input rows / output rows (fp32, [row][col])
   __shared__ float wmax[H3_NW][NC];
   __shared__ int sx[NC];                                                // the planes' column scale exponents
@@ -131,8 +141,8 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
       const float v = k < 16 ? tmp[k * NC + c] : 0.f;
       const _Float16 h = (_Float16)(v * Sc);
       const _Float16 l = (_Float16)__builtin_fmaf(v, Sc, -(float)h);
-      pl[0][c * H3_LD + k] = __builtin_bit_cast(uint16_t, h);
-      pl[1][c * H3_LD + k] = __builtin_bit_cast(uint16_t, l);
+      pl[0][0][c * H3_LD + k] = __builtin_bit_cast(uint16_t, h);
+      pl[0][1][c * H3_LD + k] = __builtin_bit_cast(uint16_t, l);
     }
     sx[c] = e;
   }
@@ -142,6 +152,8 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
   auto layer = [&](auto nksc, int l, const u32x4 (&wr)[decltype(nksc)::value][2]) {
     constexpr int NKS = decltype(nksc)::value;
     const FcLayer& L = a.L[l];
+    const uint16_t* inh = pl[cur][0];
+    const uint16_t* inl = pl[cur][1];
     float bias[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
@@ -153,8 +165,8 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
         const int col = cb * 16 + li;
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(pl[0] + col * H3_LD + ks * 32 + 8 * g);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(pl[1] + col * H3_LD + ks * 32 + 8 * g);
+        const u32x4 xh = *reinterpret_cast<const u32x4*>(inh + col * H3_LD + ks * 32 + 8 * g);
+        const u32x4 xl = *reinterpret_cast<const u32x4*>(inl + col * H3_LD + ks * 32 + 8 * g);
         acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
       }
     const int sw = ldc(L.Aexp);
@@ -162,7 +174,7 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
     float v[NCB][4];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
-      const int e = -(sw + sx[cb * 16 + li]);
+      const int e = -(sw + ((FIXS && l > 0) ? SFIX : sx[cb * 16 + li]));
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
     }
@@ -178,29 +190,45 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
         for (int cb = 0; cb < NCB; ++cb) v[cb][r] = fc_act_f<ACT>(v[cb][r] + bias[r], sp);
       }
     }
-    // column maxima: the 4 rows of a lane, the 4 lane groups of a column (shuffles), the 8 waves (LDS)
+    if constexpr (FIXS) {
+      // the other buffer: no wave reads it in this layer, and the barrier below orders it before the next layer
+      const int nb = cur ^ 1;
+      const float Sf = __builtin_amdgcn_ldexpf(1.f, SFIX);
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      float m = fmaxf(fmaxf(fabsf(v[cb][0]), fabsf(v[cb][1])), fmaxf(fabsf(v[cb][2]), fabsf(v[cb][3])));
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      if (g == 0) wmax[w][cb * 16 + li] = m;
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + li;
+        uint2 h, lo;
+        split4(v[cb], Sf, h, lo);
+        *reinterpret_cast<uint2*>(pl[nb][0] + col * H3_LD + 16 * w + 4 * g) = h;
+        *reinterpret_cast<uint2*>(pl[nb][1] + col * H3_LD + 16 * w + 4 * g) = lo;
+      }
+      __syncthreads();
+      cur = nb;
+    } else {
+      // column maxima: the 4 rows of a lane, the 4 lane groups of a column (shuffles), the 8 waves (LDS)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        float m = fmaxf(fmaxf(fabsf(v[cb][0]), fabsf(v[cb][1])), fmaxf(fabsf(v[cb][2]), fabsf(v[cb][3])));
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0) wmax[w][cb * 16 + li] = m;
+      }
+      __syncthreads();                                 // (also: every wave is done reading this layer's input planes)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + li;
+        float m = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < H3_NW; ++ww) m = fmaxf(m, wmax[ww][col]);
+        const int e = (SIN && cb == 0) ? SFIX : h3_scale_exp(m);   // (JAC: the primal column as the FWD kernel)
+        uint2 h, lo;
+        split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
+        *reinterpret_cast<uint2*>(pl[0][0] + col * H3_LD + 16 * w + 4 * g) = h;
+        *reinterpret_cast<uint2*>(pl[0][1] + col * H3_LD + 16 * w + 4 * g) = lo;
+        if (w == 0 && g == 0) sx[col] = e;
+      }
+      __syncthreads();
     }
-    __syncthreads();                                   // (also: every wave is done reading this layer's input planes)
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const int col = cb * 16 + li;
-      float m = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < H3_NW; ++ww) m = fmaxf(m, wmax[ww][col]);
-      const int e = h3_scale_exp(m);
-      uint2 h, lo;
-      split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
-      *reinterpret_cast<uint2*>(pl[0] + col * H3_LD + 16 * w + 4 * g) = h;
-      *reinterpret_cast<uint2*>(pl[1] + col * H3_LD + 16 * w + 4 * g) = lo;
-      if (w == 0 && g == 0) sx[col] = e;
-    }
-    __syncthreads();
   };
   // hidden layers: the next layer's weights are requested while this one runs (PREF, FWD: one workgroup per CU); the
   // two-per-CU JAC requests each layer's at its start (its co-resident workgroup covers the latency)
@@ -233,11 +261,11 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const u32x4 xh = *reinterpret_cast<const u32x4*>(pl[0] + col * H3_LD + ks * 32 + 8 * g);
-      const u32x4 xl = *reinterpret_cast<const u32x4*>(pl[1] + col * H3_LD + ks * 32 + 8 * g);
+      const u32x4 xh = *reinterpret_cast<const u32x4*>(pl[cur][0] + col * H3_LD + ks * 32 + 8 * g);
+      const u32x4 xl = *reinterpret_cast<const u32x4*>(pl[cur][1] + col * H3_LD + ks * 32 + 8 * g);
       acc = mfma3(wo[ks], xh, xl, acc);
     }
-    const int e = -(ldc(L.Aexp) + sx[col]);
+    const int e = -(ldc(L.Aexp) + (FIXS ? SFIX : sx[col]));
 #pragma unroll
     for (int r = 0; r < 4; ++r) tmp[(4 * g + r) * NC + col] = __builtin_amdgcn_ldexpf(acc[r], e);
   }
