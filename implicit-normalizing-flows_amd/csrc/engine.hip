@@ -325,6 +325,8 @@ FcArgs fc_args(const InfNet* n, const float* x, int B) {
   f.B = B;
   f.act = n->L[0].act;
   const bool h3 = n->mfma_mode == INF_MFMA_F16X3 && n->fch;
+  f.tan_fixed = 1;
+  for (const WLayer& w : n->L) f.tan_fixed &= w.coeff <= 1.f;
   for (int l = 0; l < f.nl && l < FC_MAXL; ++l) {
     f.L[l].A = n->L[l].f.A;
     f.L[l].Ah = h3 ? n->fch + n->fch_off[l] : nullptr;

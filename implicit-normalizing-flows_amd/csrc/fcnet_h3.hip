@@ -73,7 +73,8 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
   // the waves was ~12 % of the launch), and with two plane buffers one barrier per layer.  The JAC primal column takes
   // the same scale, so that it keeps the FWD kernel's bits (x_embed).  Its tangent columns t_l = D_l W_l t_(l-1),
   // t_0 a unit vector, |D| = |cos| <= 1, have |t_l| <= ||t_l||_2 <= prod ||W_i||_2 <= coeff^l < 1 for the Lipschitz-
-  // normalised weights: 2^SFIXT leaves a 16x margin below fp16 overflow, and the split keeps 22 bits of every element
+  // normalised weights (any induced norm: |t| <= ||t||_p, |D| <= 1 keeps each layer's bound; a.tan_fixed: every
+  // layer's coeff <= 1): 2^SFIXT leaves a 16x margin below fp16 overflow, and the split keeps 22 bits of every element
   // down to 2^-15 (an absolute error under 2^-36 below that).  No column maxima in the JAC either then (one barrier
   // per layer stays: the planes are single-buffered at two workgroups per CU).
   constexpr bool SIN = ACT == ACT_SIN;
@@ -209,7 +210,7 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
       }
       __syncthreads();
       cur = nb;
-    } else if constexpr (SIN) {
+    } else if (SIN && a.tan_fixed) {
       __syncthreads();                                 // every wave is done reading this layer's input planes
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
@@ -238,7 +239,7 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
         float m = 0.f;
 #pragma unroll
         for (int ww = 0; ww < H3_NW; ++ww) m = fmaxf(m, wmax[ww][col]);
-        const int e = h3_scale_exp(m);
+        const int e = (SIN && cb == 0) ? SFIX : h3_scale_exp(m);   // (JAC: the primal column as the FWD kernel)
         uint2 h, lo;
         split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
         *reinterpret_cast<uint2*>(pl[0][0] + col * H3_LD + 16 * w + 4 * g) = h;

@@ -258,6 +258,9 @@ struct FcArgs {
   const float* lp_in;
   const float* lp_ldx;
   float* lp_out;
+  // JAC of Sin nets on the f16x3 kernels: every layer's Lipschitz cap coeff <= 1, so the tangent columns stay in [-1, 1]
+  // and take one fixed scale (fcnet_h3.hip); else per-column maxima
+  int tan_fixed;
 };
 int fcnet_supported(const FcArgs& a, bool jac);
 int launch_fcnet(const FcArgs& a, bool jac, hipStream_t s);

@@ -219,12 +219,13 @@ def _fp64_net_and_logdet(sd, prefix, info, coeff, x):
     return y, torch.logdet(eye + J)
 
 
-@pytest.mark.parametrize('arch', [syn.POWER, syn.TOY], ids=['power', 'toy'])
+@pytest.mark.parametrize('arch', [syn.POWER, syn.TOY, dict(syn.POWER, coeff=1.2)], ids=['power', 'toy', 'power_coeff1.2'])
 def test_fc_f16x3_error_at_fp32_level(arch):
     """The fused fc kernels' f16x3 arithmetic (fcnet_h3.hip: forward, forward-mode Jacobian + LU log-det) and the block
     kernel's x-branch log-det (fcblock.hip, which also evaluates the Sin activation by its short polynomial form)
     against an fp64 evaluation of the same net, next to the exact fp32 MFMA kernels (fcnet.hip): errors relative to
-    max(1, max|ref|) within 2x the fp32 kernels' + 2e-7, and all within 2e-6."""
+    max(1, max|ref|) within 2x the fp32 kernels' + 2e-7, and all within 2e-6.  coeff 1.2: the Jacobian's tangent
+    columns on per-column scales (FcArgs::tan_fixed 0) instead of the fixed one."""
     B = 1000
     m, sd = _model(arch, B)
     blk = imblocks(m)[0]
