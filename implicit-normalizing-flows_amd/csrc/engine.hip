@@ -510,8 +510,9 @@ int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const
     return INF_OK;
   }
   if (!direct && !ps_on) {                            // global rule: the reduction writes the sums into the slot
-    INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, sl->host, s));
-    INF_HIP(hipEventRecord(sl->ev, s));
+    bool bound = false;                              // (and completes the slot's event itself: no marker packet)
+    INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, sl->host, s, sl->ev, &bound));
+    if (!bound) INF_HIP(hipEventRecord(sl->ev, s));
     return INF_OK;
   }
   if (!direct) INF_TRY(launch_reduce_partials(bf.part, B, f->fc ? 1 : bf.nchunk, bf.sumsq, s));

@@ -333,7 +333,15 @@ __global__ void reduce_partials_kernel(const double* partial, int batch, int nch
   for (int c = 0; c < nchunk; ++c) s += partial[(long)b * nchunk + c];
   out[b] = s;
 }
-int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s) {
+int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s, hipEvent_t stop_ev,
+                           bool* stop_bound) {
+  if (stop_ev && !prof_enabled()) {            // the readback event completes with the launch itself
+    hipExtLaunchKernelGGL(reduce_partials_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, nullptr, stop_ev, 0,
+                          partial, batch, nchunk, out);
+    INF_CHECK_LAUNCH();
+    *stop_bound = true;
+    return INF_OK;
+  }
   INF_PROF_LAUNCH(s, 705, 8.0 * batch * nchunk + 8.0 * batch, reduce_partials_kernel, dim3((batch + 255) / 256),
                   dim3(256), 0, s, partial, batch, nchunk, out);
   return INF_OK;
