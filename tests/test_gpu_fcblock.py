@@ -324,3 +324,47 @@ def test_chain_call_matches_block_by_block(convergence, fc_block, monkeypatch):
     for a, b in zip(st_c, st_b):
         for k in ('nstep', 'lowest_step', 'prot_break', 'trace', 'sample_nstep'):
             assert a.get(k) == b.get(k), k
+
+
+@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
+def test_chain_with_protective_break_matches_block_by_block(golden_dir, convergence, monkeypatch):
+    """A chain whose first block breaks (PROT_BREAK_DEEP nets, the reference's prot_break_deep_b6 input) followed by
+    two POWER-shaped blocks: the breaking block recomputes z on its own, so the next block runs its own x-branch
+    launch instead of the pair; the blocks after it pair up again.  The chain call against the blocks one by one:
+    bitwise the same z and log p, the same statistics per block."""
+    import lib.layers.imblock as imb
+    from lib.layers.flows import SequentialFlow
+    g, x = _load_prot_break_deep(golden_dir)
+    B = x.shape[0]
+    power = _model(syn.POWER, B)[0]
+    blocks = [_prot_break_deep_block(), imblocks(power)[0], imblocks(power)[1]]
+    for b in blocks:
+        b.convergence = convergence
+    flow = SequentialFlow(blocks).to(DEV).eval()
+    tabular_logpx(flow, x)                                   # builds the engine nets
+    calls = []
+    real = imb.eval_exact_chain
+
+    def spy(*a, **k):
+        out = real(*a, **k)
+        calls.append(out is not None)
+        return out
+    monkeypatch.setattr(imb, 'eval_exact_chain', spy)
+    _hip.profile_begin(20000)
+    try:
+        _, lp_c, z_c = tabular_logpx(flow, x)
+        torch.cuda.synchronize()
+    finally:
+        launches = {s_['tag']: s_['launches'] for s_ in _hip.profile_end()}
+    st_c = [dict(b.last_broyden) for b in blocks]
+    assert calls == [True]
+    assert st_c[0]['prot_break'], st_c[0]
+    monkeypatch.setattr(imb, 'eval_exact_chain', lambda *a, **k: None)
+    _, lp_b, z_b = tabular_logpx(flow, x)
+    st_b = [dict(b.last_broyden) for b in blocks]
+    assert torch.equal(z_c, z_b) and torch.equal(lp_c, lp_b)
+    for a, b in zip(st_c, st_b):
+        for k in ('nstep', 'lowest_step', 'prot_break', 'fixed_point_iters', 'trace', 'sample_nstep'):
+            assert a.get(k) == b.get(k), k
+    if convergence == 'global' and not st_c[1]['prot_break']:   # (per sample: every block on the block kernel)
+        assert launches.get(602, 0) >= 1, launches             # blocks 1 -> 2 in one grid
