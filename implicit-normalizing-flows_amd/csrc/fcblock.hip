@@ -247,26 +247,48 @@ __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, cons
         for (int cb = 0; cb < NCB; ++cb) v[cb][r] = fc_act_f<ACT>(v[cb][r] + bias[r], sp);
       }
     }
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      float m = fmaxf(fmaxf(fabsf(v[cb][0]), fabsf(v[cb][1])), fmaxf(fabsf(v[cb][2]), fabsf(v[cb][3])));
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      if (g == 0) P.wmax[w * NC + cb * 16 + li] = m;
+    // Sin nets: the fixed scales of fcnet_h3.hip (the forward and primal values in [-1/(2 pi), 1/(2 pi)], the tangents
+    // bounded by the Lipschitz caps where every coeff <= 1) -- no column-max exchange; else per-column maxima.  (The
+    // transposed passes of the series keep per-column scales: their vectors carry the probe's norm.)
+    bool allfix = false;
+    if constexpr (ACT == ACT_SIN && SV != SV_VJP) {
+      if constexpr (JAC) allfix = a.tan_fixed != 0;
+      else allfix = true;
     }
-    bk_sync();
+    if (allfix) {
+      bk_sync();                                 // every wave is done reading this layer's input planes
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const int col = cb * 16 + li;
-      float m = 0.f;
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + li;
+        const int e = (JAC && cb > 0) ? FC_SFIXT : FC_SFIX;
+        uint2 h, lo;
+        split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
+        *reinterpret_cast<uint2*>(P.pl0 + col * BK_LD + 16 * w + 4 * g) = h;
+        *reinterpret_cast<uint2*>(P.pl1 + col * BK_LD + 16 * w + 4 * g) = lo;
+        if (w == 0 && g == 0) P.sx[col] = e;
+      }
+    } else {
 #pragma unroll
-      for (int ww = 0; ww < BK_NW; ++ww) m = fmaxf(m, P.wmax[ww * NC + col]);
-      const int e = h3_scale_exp(m);
-      uint2 h, lo;
-      split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
-      *reinterpret_cast<uint2*>(P.pl0 + col * BK_LD + 16 * w + 4 * g) = h;
-      *reinterpret_cast<uint2*>(P.pl1 + col * BK_LD + 16 * w + 4 * g) = lo;
-      if (w == 0 && g == 0) P.sx[col] = e;
+      for (int cb = 0; cb < NCB; ++cb) {
+        float m = fmaxf(fmaxf(fabsf(v[cb][0]), fabsf(v[cb][1])), fmaxf(fabsf(v[cb][2]), fabsf(v[cb][3])));
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0) P.wmax[w * NC + cb * 16 + li] = m;
+      }
+      bk_sync();
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = cb * 16 + li;
+        float m = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < BK_NW; ++ww) m = fmaxf(m, P.wmax[ww * NC + col]);
+        const int e = (ACT == ACT_SIN && SV != SV_VJP && cb == 0) ? FC_SFIX : h3_scale_exp(m);
+        uint2 h, lo;
+        split4(v[cb], __builtin_amdgcn_ldexpf(1.f, e), h, lo);
+        *reinterpret_cast<uint2*>(P.pl0 + col * BK_LD + 16 * w + 4 * g) = h;
+        *reinterpret_cast<uint2*>(P.pl1 + col * BK_LD + 16 * w + 4 * g) = lo;
+        if (w == 0 && g == 0) P.sx[col] = e;
+      }
     }
     bk_sync();
     BK_STAMP(ts);
@@ -394,24 +416,32 @@ __device__ __forceinline__ void mlp_jac2(const FcArgs& a, const Pass& P, Stamps*
 #pragma unroll
         for (int j = 1; j < NJ; ++j) v[t][j][r] *= dd;
       }
+    const bool allfix = ACT == ACT_SIN && a.tan_fixed;   // (mlp_pass's fixed scales)
+    if (!allfix) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float m = 0.f;
+      for (int j = 0; j < NJ; ++j) {
+        float m = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[t][j][0]), fabsf(v[t][j][1])), fmaxf(fabsf(v[t][j][2]), fabsf(v[t][j][3]))));
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      if (g == 0 && (j > 0 || cg == 0)) P.wmax[rg * NC + cbof(j) * 16 + li] = m;
+        for (int t = 0; t < 2; ++t)
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v[t][j][0]), fabsf(v[t][j][1])), fmaxf(fabsf(v[t][j][2]), fabsf(v[t][j][3]))));
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0 && (j > 0 || cg == 0)) P.wmax[rg * NC + cbof(j) * 16 + li] = m;
+      }
     }
     bk_sync();
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       if (j == 0 && cg != 0) continue;           // the primal's planes come from column group 0
       const int col = cbof(j) * 16 + li;
-      const float m = fmaxf(fmaxf(P.wmax[0 * NC + col], P.wmax[1 * NC + col]),
-                            fmaxf(P.wmax[2 * NC + col], P.wmax[3 * NC + col]));
-      const int e = h3_scale_exp(m);
+      int e;
+      if (allfix) {
+        e = j == 0 ? FC_SFIX : FC_SFIXT;
+      } else {
+        const float m = fmaxf(fmaxf(P.wmax[0 * NC + col], P.wmax[1 * NC + col]),
+                              fmaxf(P.wmax[2 * NC + col], P.wmax[3 * NC + col]));
+        e = (ACT == ACT_SIN && j == 0) ? FC_SFIX : h3_scale_exp(m);
+      }
       const float S2 = __builtin_amdgcn_ldexpf(1.f, e);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {

@@ -177,6 +177,11 @@ __device__ __forceinline__ float logdet_lu(F J) {
   return sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
 }
 
+// Fixed power-of-two scales of the f16x3 fc kernels for Sin nets (fcnet_h3.hip explains the bounds): the forward /
+// primal hidden values (|v| <= 1 / (2 pi)) and the forward-mode tangents (|t| <= 1 where every layer's coeff <= 1)
+constexpr int FC_SFIX = 17;
+constexpr int FC_SFIXT = 12;
+
 // The hidden activations of the f16x3 fc kernels (fcnet_h3.hip, fcblock.hip) in short inline forms: the precise sinf /
 // cosf expand to hundreds of instructions per call (out of the block kernel's instruction cache, and most of the VALU
 // of the latency-bound FWD / JAC launches), the precise swish two IEEE divisions and a range-reduced expf.  Sin (activations.py:7-12): sin(2 pi a) / (2 pi) and its

@@ -79,8 +79,8 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
   // per layer stays: the planes are single-buffered at two workgroups per CU).
   constexpr bool SIN = ACT == ACT_SIN;
   constexpr bool FIXS = SIN && !JAC;
-  constexpr int SFIX = 17;
-  constexpr int SFIXT = 12;
+  constexpr int SFIX = FC_SFIX;
+  constexpr int SFIXT = FC_SFIXT;
   constexpr int NBUF = FIXS ? 2 : 1;
   __shared__ __attribute__((aligned(16))) uint16_t pl[NBUF][2][NC * H3_LD];   // activation planes h, l: [col][k]
   int cur = 0;                                                              // the buffer holding the layer input
