@@ -10,7 +10,7 @@ cp $L /tmp/libinflow_base.so
 for rep in 1 2; do
   for v in base "$@"; do
     if [ $v = base ]; then cp /tmp/libinflow_base.so $L; else cp altlib/lib_$v.so $L; fi
-    timeout -k 10 200 python bench.py --config power --cpu-baseline 0 --steps 40 --warmup 5 > $O/$v.$rep.json 2>/dev/null
+    timeout -k 10 200 python bench.py --config ${CFG:-power} --cpu-baseline 0 --steps 40 --warmup 5 > $O/$v.$rep.json 2>/dev/null
     python -c "import json;d=json.loads(open('$O/$v.$rep.json').read().strip().splitlines()[-1]);print('$v', d['value'], d['ms_per_step'])"
   done
 done
