@@ -469,9 +469,9 @@ struct SumsSlot {
   hipEvent_t ev = nullptr;
   int cap = 0;
 };
+static thread_local SumsSlot g_sums_slots[2];
 static int sums_slot(int i, int B, SumsSlot** out) {
-  static thread_local SumsSlot slots[2];
-  SumsSlot& sl = slots[i & 1];
+  SumsSlot& sl = g_sums_slots[i & 1];
   if (sl.cap < B + 1) {
     if (sl.host) (void)hipHostFree(sl.host);
     sl.host = nullptr;
@@ -1090,6 +1090,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
 // statistics; a protective break runs the Banach fallback and the recompute on the host path (as below).
 static thread_local char* g_bk_host = nullptr;
 static thread_local size_t g_bk_host_cap = 0;
+static thread_local hipEvent_t g_bk_ev = nullptr;
 int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B, int T,
                   double eps_in, InfBroydenStats* stats, Bufs& bf, hipStream_t s) {
   if (nx->mfma_mode != INF_MFMA_F16X3 || nz->mfma_mode != INF_MFMA_F16X3 || !bf.bk_sync) return INF_ERR_UNSUPPORTED;
@@ -1139,12 +1140,8 @@ int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logde
   }
   INF_HIP(hipMemcpyAsync(g_bk_host, bf.bk_sync, 16, hipMemcpyDeviceToHost, s));
   INF_HIP(hipMemcpyAsync(g_bk_host + 16, bf.bk_out, nbytes, hipMemcpyDeviceToHost, s));
-  hipEvent_t ev = nullptr;
-  {
-    static thread_local hipEvent_t bk_ev = nullptr;
-    if (!bk_ev && hipEventCreateWithFlags(&bk_ev, INF_EV_SYNC) != hipSuccess) return INF_ERR_HIP;
-    ev = bk_ev;
-  }
+  if (!g_bk_ev && hipEventCreateWithFlags(&g_bk_ev, INF_EV_SYNC) != hipSuccess) return INF_ERR_HIP;
+  hipEvent_t ev = g_bk_ev;
   INF_HIP(hipEventRecord(ev, s));
   INF_TRY(host_wait(ev));
   if (*reinterpret_cast<unsigned*>(g_bk_host) != 0) {
@@ -1967,11 +1964,11 @@ struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
+static thread_local SideStream g_side[16];
 static SideStream* side_stream() {
-  static thread_local SideStream per_dev[16];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  SideStream& ss = per_dev[dev];
+  SideStream& ss = g_side[dev];
   if (!ss.s) {
     if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&ss.fork, INF_EV_SYNC) != hipSuccess ||
@@ -2235,7 +2232,10 @@ size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int ba
 int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_blocks, const float* x, float* z,
                               const float* logp_in, float* logp_out, int B, const int* thresholds, const double* eps,
                               InfBroydenStats* stats, void* ws, size_t ws_bytes, void* stream) {
-  if (!net_x || !net_z || n_blocks <= 0 || !x || !z || !logp_out || B <= 0 || !thresholds || !eps || x == z)
+  // logp_in == logp_out is refused: a block's log-density step is folded into its z-branch launch, which runs again
+  // when the predicted last iterate was not the result, and would then read the already-updated log p
+  if (!net_x || !net_z || n_blocks <= 0 || !x || !z || !logp_out || B <= 0 || !thresholds || !eps || x == z ||
+      logp_in == logp_out)
     return INF_ERR_INVALID;
   for (int i = 0; i < n_blocks; ++i) {
     InfNet *nx = net_x[i], *nz = net_z[i];
@@ -2327,6 +2327,8 @@ static int fc_series(InfNet* const* nets, const float* const* xs, const float* c
       f.b = n->L[l].b;
       f.beta = n->L[l].act_beta;
       FcLayer& t = a.t[i].L[l];
+      t.A = n->L[a.nl - 1 - l].g.A;                 // W_{nl-1-l}^T fp32 (the input layer's exact contraction)
+      t.Kpad = n->L[a.nl - 1 - l].g.Kpad;
       t.Ah = n->fcht + n->fch_off[l];
       t.Aexp = n->fchtexp + l;
     }
@@ -2599,6 +2601,48 @@ int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, co
   ba.m = (nstep - 1) % T;
   ba.ncols = std::min(nstep, T);
   return launch_broyden_update(ba, (hipStream_t)stream);
+}
+
+// ---- teardown ---------------------------------------------------------------------------------
+// The calling thread's engine-held host resources: the pinned readback slots and their events, the block kernel's
+// statistics buffer and event, the side streams and their fork / join events, the profiling events.  They were kept
+// for the process lifetime and left to the HIP runtime's own exit-time teardown; releasing them before it (lib/_hip
+// registers this with atexit) leaves that teardown nothing of ours.  Waits for the device first.  Idempotent; nets stay
+// valid and the next call re-creates what it needs.
+int inf_shutdown(void) {
+  int rc = INF_OK;
+  if (hipDeviceSynchronize() != hipSuccess) rc = INF_ERR_HIP;
+  for (SumsSlot& sl : g_sums_slots) {
+    if (sl.host) (void)hipHostFree(sl.host);
+    if (sl.ev) (void)hipEventDestroy(sl.ev);
+    sl = SumsSlot{};
+  }
+  if (g_bk_host) (void)hipHostFree(g_bk_host);
+  g_bk_host = nullptr;
+  g_bk_host_cap = 0;
+  if (g_bk_ev) (void)hipEventDestroy(g_bk_ev);
+  g_bk_ev = nullptr;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (int dev = 0; dev < 16; ++dev) {
+    SideStream& ss = g_side[dev];
+    if (!ss.s) continue;
+    (void)hipSetDevice(dev);
+    (void)hipStreamSynchronize(ss.s);
+    if (ss.fork) (void)hipEventDestroy(ss.fork);
+    if (ss.join) (void)hipEventDestroy(ss.join);
+    (void)hipStreamDestroy(ss.s);
+    ss = SideStream{};
+  }
+  (void)hipSetDevice(cur);
+  for (auto& p : g_prof) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  g_prof.clear();
+  g_prof_used = 0;
+  g_prof_on = false;
+  return rc;
 }
 
 // ---- launch timing --------------------------------------------------------------------------

@@ -94,25 +94,30 @@ __device__ __forceinline__ void split4(const float (&v)[4], float S, uint2& h, u
   l = make_uint2(__builtin_bit_cast(unsigned, c), __builtin_bit_cast(unsigned, e));
 }
 
-// A net's resident weights for the solve: the hidden layers' fragments of wave w in registers; the input layer (one k
-// step, all row tiles) and the output layer (four k steps, row tile 0) as fragment planes in LDS (24 KiB at 128 wide)
+// A net's resident weights for the solve: the hidden layers' fragments of wave w in registers; the input layer's fp32
+// rows (exact VALU contraction, fcnet_common.h fc_in_col; [row][BK_W0_LD], k >= d zero) and the output layer (four k
+// steps, row tile 0) as fragment planes in LDS (12 KiB at 128 wide)
 template <int NH>
 struct NetRegs {
   u32x4 wh[NH][4][2];
-  const u32x4* w0;   // LDS: [(rt * 2 + plane) * 64 + lane], rt < 8
+  const float* w0;   // LDS: [row * BK_W0_LD + k], row < 128, k < d
   const u32x4* wo;   // LDS: [(ks * 2 + plane) * 64 + lane], ks < 4
 };
-constexpr int BK_W0_VEC = 8 * 2 * 64;     // u32x4 of the input layer's planes
+constexpr int BK_W0_LD = 8;               // floats per input-layer row in LDS (d <= 8)
+constexpr int BK_W0_VEC = FC_H * BK_W0_LD / 4;   // u32x4 of the input layer's fp32 rows
 constexpr int BK_WO_VEC = 4 * 2 * 64;     // u32x4 of the output layer's planes
 template <int NH>
 __device__ __forceinline__ void load_net(const FcArgs& a, int w, int lane, u32x4* lds_w, NetRegs<NH>& r) {
-  const u32x4* g0 = reinterpret_cast<const u32x4*>(a.L[0].Ah);
   const u32x4* go = reinterpret_cast<const u32x4*>(a.L[NH + 1].Ah);
-  for (int i = threadIdx.x; i < BK_W0_VEC + BK_WO_VEC; i += BK_NT)
-    lds_w[i] = i < BK_W0_VEC ? g0[i] : go[i - BK_W0_VEC];
+  float* w0 = reinterpret_cast<float*>(lds_w);
+  for (int i = threadIdx.x; i < FC_H * BK_W0_LD; i += BK_NT) {
+    const int row = i / BK_W0_LD, k = i - row * BK_W0_LD;
+    w0[i] = k < a.d ? a.L[0].A[(long)row * a.L[0].Kpad + k] : 0.f;
+  }
+  for (int i = threadIdx.x; i < BK_WO_VEC; i += BK_NT) lds_w[BK_W0_VEC + i] = go[i];
 #pragma unroll
   for (int l = 0; l < NH; ++l) ldw<4>(a.L[1 + l].Ah, 4, w, lane, r.wh[l]);
-  r.w0 = lds_w;
+  r.w0 = w0;
   r.wo = lds_w + BK_W0_VEC;
 }
 
@@ -132,71 +137,30 @@ struct Pass {
   int* sx;         // column scale exponents
 };
 
-// The input rows of a pass (tmp rows [0, 16), fp32 [row][col]) as the first layer's operand planes: per column its scale
-// exponent (the max over the rows) and the split of rows [0, 32) (rows >= 16: the K padding), written 16 bytes at a time
-template <int NC>
-__device__ __forceinline__ void split_input(const Pass& P) {
-  for (int c = threadIdx.x; c < NC; c += BK_NT) {
-    float v[16];
-    float m = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      v[k] = P.tmp[k * NC + c];
-      m = fmaxf(m, fabsf(v[k]));
-    }
-    const int e = h3_scale_exp(m);
-    const float Sc = __builtin_amdgcn_ldexpf(1.f, e);
-    u32x4 hq[2], lq[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float a0 = v[8 * q + 2 * j], a1 = v[8 * q + 2 * j + 1];
-        const _Float16 h0 = (_Float16)(a0 * Sc), h1 = (_Float16)(a1 * Sc);
-        const _Float16 l0 = (_Float16)__builtin_fmaf(a0, Sc, -(float)h0);
-        const _Float16 l1 = (_Float16)__builtin_fmaf(a1, Sc, -(float)h1);
-        const f16x2 hv = {h0, h1}, lv = {l0, l1};
-        hq[q][j] = __builtin_bit_cast(unsigned, hv);
-        lq[q][j] = __builtin_bit_cast(unsigned, lv);
-      }
-    u32x4* ph = reinterpret_cast<u32x4*>(P.pl0 + c * BK_LD);
-    u32x4* pl = reinterpret_cast<u32x4*>(P.pl1 + c * BK_LD);
-    const u32x4 zero = {0u, 0u, 0u, 0u};
-    ph[0] = hq[0];
-    ph[1] = hq[1];
-    ph[2] = zero;
-    ph[3] = zero;
-    pl[0] = lq[0];
-    pl[1] = lq[1];
-    pl[2] = zero;
-    pl[3] = zero;
-    P.sx[c] = e;
-  }
-}
-
 // One pass of the net over NC = 16 NCB columns: inputs in tmp rows [0, 16) (rows >= d zero), the output layer's sums
-// (no bias) left in tmp rows [0, 16).  The arithmetic of fcnet_h3.hip per column: scaled two-piece fp16 operands, three
-// products per fp32 product on v_mfma_f32_16x16x32_f16, fp32 accumulation, exact unscale.  JAC: column block 0 is the
+// (no bias) left in tmp rows [0, 16).  The arithmetic of fcnet_h3.hip per column: the input layer (K = DD) in exact fp32
+// on the VALU from the fp32 rows, the others scaled two-piece fp16 operands, three products per fp32 product on
+// v_mfma_f32_16x16x32_f16, fp32 accumulation, exact unscale.  JAC: column block 0 is the
 // primal, the others are tangents, multiplied by act'(pre-activation of the primal).  REG: the weights come from
 // registers (loaded once per solve) instead of global memory.  SV_SAVE: a forward pass that also keeps act' of
 // every hidden unit in D (registers: wave w holds rows 16 w + 4 g + r of every hidden layer); SV_VJP: the pass of the
 // transposed net (a.L[j] = W_{L-1-j}^T, fcseries_kernel) whose hidden epilogue is the product with D's derivatives of
 // forward layer NH - j instead of bias + activation -- the row ownership of both passes is the same.
-template <int NCB, bool JAC, int ACT, int NH, bool REG, int SV = SV_NONE, class NA = FcArgs>
+template <int DD, int NCB, bool JAC, int ACT, int NH, bool REG, int SV = SV_NONE, class NA = FcArgs>
 __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, const Pass& P, Stamps* ts,
                                          Derivs<NH, NCB>* D = nullptr) {
   constexpr int NC = 16 * NCB;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
   u32x4 wnext[4][2];
-  u32x4 w0[1][2];
+  u32x4 w0[1][2];                              // (unused: the input layer is the VALU contraction)
+  float wi[4][DD];
   if constexpr (!REG) {
-    ldw<1>(a.L[0].Ah, 1, w, lane, w0);
+    fc_in_weights<DD>(a.L[0].A, a.L[0].Kpad, DD, 16 * w + 4 * g, wi);
     if (NH > 0) ldw<4>(a.L[1].Ah, 4, w, lane, wnext);
   }
-  bk_sync();                                   // the caller's input rows
-  split_input<NC>(P);
-  bk_sync();
+  bk_sync();                                   // the caller's input rows (and, REG, the resident weights)
+  if constexpr (REG) fc_in_weights<DD>(R->w0, BK_W0_LD, DD, 16 * w + 4 * g, wi);
   BK_STAMP(ts);
 
   auto layer = [&](auto nksc, int l, const u32x4 (&wr)[decltype(nksc)::value][2]) {
@@ -207,26 +171,31 @@ __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
     }
-    f32x4 acc[NCB];
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const int col = cb * 16 + li;
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(P.pl0 + col * BK_LD + ks * 32 + 8 * g);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(P.pl1 + col * BK_LD + ks * 32 + 8 * g);
-        acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
-      }
-    const int sw = ldc(L.Aexp);
     const float sp = (ACT == ACT_SWISH && SV != SV_VJP) ? softplus_f(ldc(L.beta)) : 0.f;
     float v[NCB][4];
+    if constexpr (NKS == 1) {
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const int e = -(sw + P.sx[cb * 16 + li]);
+      for (int cb = 0; cb < NCB; ++cb) fc_in_col<DD>(wi, P.tmp + cb * 16 + li, NC, DD, v[cb]);
+    } else {
+      f32x4 acc[NCB];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
+      for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int col = cb * 16 + li;
+          const u32x4 xh = *reinterpret_cast<const u32x4*>(P.pl0 + col * BK_LD + ks * 32 + 8 * g);
+          const u32x4 xl = *reinterpret_cast<const u32x4*>(P.pl1 + col * BK_LD + ks * 32 + 8 * g);
+          acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
+        }
+      const int sw = ldc(L.Aexp);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int e = -(sw + P.sx[cb * 16 + li]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -294,12 +263,7 @@ __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, cons
     BK_STAMP(ts);
   };
   if constexpr (REG) {
-    {
-      u32x4 wi[1][2];
-      wi[0][0] = R->w0[(w * 2 + 0) * 64 + lane];
-      wi[0][1] = R->w0[(w * 2 + 1) * 64 + lane];
-      layer(std::integral_constant<int, 1>(), 0, wi);
-    }
+    layer(std::integral_constant<int, 1>(), 0, w0);
 #pragma unroll
     for (int l = 0; l < NH; ++l) layer(std::integral_constant<int, 4>(), 1 + l, R->wh[l]);
   } else {
@@ -350,7 +314,7 @@ __device__ __forceinline__ void mlp_pass(const NA& a, const NetRegs<NH>* R, cons
 // column block 0 and tangent blocks [1 + c NT / 2, 1 + (c + 1) NT / 2) (the primal is computed by both groups: each
 // needs act' of its rows).  The arithmetic per column is mlp_pass's (same products, same order, same scales); weights
 // stream from global memory, each layer's requested right after the previous layer's products.
-template <int NCB, int ACT, int NH>
+template <int DD, int NCB, int ACT, int NH>
 __device__ __forceinline__ void mlp_jac2(const FcArgs& a, const Pass& P, Stamps* ts) {
   constexpr int NC = 16 * NCB;
   constexpr int NT = NCB - 1;                 // tangent blocks (even)
@@ -360,51 +324,57 @@ __device__ __forceinline__ void mlp_jac2(const FcArgs& a, const Pass& P, Stamps*
   const int li = lane & 15, g = lane >> 4;
   const int rg = w & 3, cg = w >> 2;
   auto cbof = [&](int j) { return j == 0 ? 0 : j + cg * (NT / 2); };
-  u32x4 wi[2][1][2];
+  u32x4 wi[2][1][2];                           // (unused: the input layer is the VALU contraction)
+  float wf[2][4][DD];
+  fc_in_weights<DD>(a.L[0].A, a.L[0].Kpad, DD, 16 * (2 * rg + 0) + 4 * g, wf[0]);
+  fc_in_weights<DD>(a.L[0].A, a.L[0].Kpad, DD, 16 * (2 * rg + 1) + 4 * g, wf[1]);
   u32x4 wh[2][4][2];
-  ldw<1>(a.L[0].Ah, 1, 2 * rg + 0, lane, wi[0]);
-  ldw<1>(a.L[0].Ah, 1, 2 * rg + 1, lane, wi[1]);
   if (NH > 0) {
     ldw<4>(a.L[1].Ah, 4, 2 * rg + 0, lane, wh[0]);
     ldw<4>(a.L[1].Ah, 4, 2 * rg + 1, lane, wh[1]);
   }
   bk_sync();                                   // the caller's input rows
-  split_input<NC>(P);
-  bk_sync();
   BK_STAMP(ts);
   auto layer = [&](auto nksc, int l, u32x4 (&wr)[2][decltype(nksc)::value][2]) {
     constexpr int NKS = decltype(nksc)::value;
     const FcLayer& L = a.L[l];
-    f32x4 acc[2][NJ];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = cbof(j) * 16 + li;
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(P.pl0 + col * BK_LD + ks * 32 + 8 * g);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(P.pl1 + col * BK_LD + ks * 32 + 8 * g);
-        acc[0][j] = mfma3(wr[0][ks], xh, xl, acc[0][j]);
-        acc[1][j] = mfma3(wr[1][ks], xh, xl, acc[1][j]);
-      }
-    // the next hidden layer's weights, in flight during this epilogue
-    if (NKS == 4 && l + 1 <= NH) {
-      ldw<4>(a.L[l + 1].Ah, 4, 2 * rg + 0, lane, wh[0]);
-      ldw<4>(a.L[l + 1].Ah, 4, 2 * rg + 1, lane, wh[1]);
-    }
-    const int sw = ldc(L.Aexp);
     const float sp = (ACT == ACT_SWISH) ? softplus_f(ldc(L.beta)) : 0.f;
     float v[2][NJ][4];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int e = -(sw + P.sx[cbof(j) * 16 + li]);
+    if constexpr (NKS == 1) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[t][j][r] = __builtin_amdgcn_ldexpf(acc[t][j][r], e);
+        for (int j = 0; j < NJ; ++j) fc_in_col<DD>(wf[t], P.tmp + cbof(j) * 16 + li, NC, DD, v[t][j]);
+    } else {
+      f32x4 acc[2][NJ];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = cbof(j) * 16 + li;
+          const u32x4 xh = *reinterpret_cast<const u32x4*>(P.pl0 + col * BK_LD + ks * 32 + 8 * g);
+          const u32x4 xl = *reinterpret_cast<const u32x4*>(P.pl1 + col * BK_LD + ks * 32 + 8 * g);
+          acc[0][j] = mfma3(wr[0][ks], xh, xl, acc[0][j]);
+          acc[1][j] = mfma3(wr[1][ks], xh, xl, acc[1][j]);
+        }
+      // the next hidden layer's weights, in flight during this epilogue
+      if (l + 1 <= NH) {
+        ldw<4>(a.L[l + 1].Ah, 4, 2 * rg + 0, lane, wh[0]);
+        ldw<4>(a.L[l + 1].Ah, 4, 2 * rg + 1, lane, wh[1]);
+      }
+      const int sw = ldc(L.Aexp);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = -(sw + P.sx[cbof(j) * 16 + li]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[t][j][r] = __builtin_amdgcn_ldexpf(acc[t][j][r], e);
+      }
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -490,34 +460,37 @@ __device__ __forceinline__ void publish(gu64* g, unsigned tag, double v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 // wave 0: the sum over workgroups (in workgroup order per lane, then a fixed butterfly: the same bits in every
-// workgroup).  Returns false on timeout.
+// workgroup).  The granules are read 512 at a time (8 per lane), in order, so any grid size is covered.  Returns false
+// on timeout.
 __device__ __forceinline__ bool gather_total(const gu64* g, unsigned tag, int nwg, int lane, double& total) {
-  const int n = 2 * nwg;        // granules; lane holds indices lane + 64 q
-  unsigned long long v[8];
-  for (unsigned spins = 0;; ++spins) {
-    bool ok = true;
+  const int n = 2 * nwg;        // granules; lane holds indices base + lane + 64 q
+  double s = 0.0;
+  for (int base = 0; base < n; base += 512) {
+    unsigned long long v[8];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = base + lane + 64 * q;
+        if (i < n) {
+          v[q] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(v[q] >> 32) == tag;
+        } else {
+          v[q] = 0;
+        }
+      }
+      if (__all(ok)) break;
+      if (spins > BK_SPIN_MAX) return false;
+      __builtin_amdgcn_s_sleep(2);
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int i = lane + 64 * q;
-      if (i < n) {
-        v[q] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok &= (unsigned)(v[q] >> 32) == tag;
-      } else {
-        v[q] = 0;
+      const unsigned lo = (unsigned)__shfl_down((int)(unsigned)v[q], 1, 64);   // the odd granule of the pair
+      const int i = base + lane + 64 * q;
+      if (!(lane & 1) && i < n) {
+        const unsigned long long bits = ((v[q] & 0xffffffffull) << 32) | lo;
+        s += __longlong_as_double((long long)bits);
       }
-    }
-    if (__all(ok)) break;
-    if (spins > BK_SPIN_MAX) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  double s = 0.0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const unsigned lo = (unsigned)__shfl_down((int)(unsigned)v[q], 1, 64);   // the odd granule of the pair
-    const int i = lane + 64 * q;
-    if (!(lane & 1) && i < n) {
-      const unsigned long long bits = ((v[q] & 0xffffffffull) << 32) | lo;
-      s += __longlong_as_double((long long)bits);
     }
   }
 #pragma unroll
@@ -696,7 +669,7 @@ __device__ __forceinline__ void bk_jacobian(const FcArgs& a, char* jbase, const 
       if (k < DD && b0 + s < B) v = cb > 0 ? (k == cb - 1 ? 1.f : 0.f) : in[s * DD + k];
       P.tmp[i] = v;
     }
-    mlp_jac2<NCB, ACT, NH>(a, P, ts);
+    mlp_jac2<DD, NCB, ACT, NH>(a, P, ts);
     if (tid < 16) {
       const int s = 16 * q + tid;
       const long b = b0 + s;
@@ -787,7 +760,7 @@ __global__ __launch_bounds__(BK_NT) void fcblock_kernel(FcBlockArgs a) {
   // f_z at the iterate in tmp rows [0, DD) (V_X holds the same values); per sample thread: f -> fcur, g -> g, the
   // sum of squares of g returned (0 elsewhere)
   auto residual = [&]() -> double {
-    mlp_pass<BK_FCB, false, ACT, NH, true>(a.nz, &R, P, ts);
+    mlp_pass<DD, BK_FCB, false, ACT, NH, true>(a.nz, &R, P, ts);
     double acc = 0.0;
     if (valid_t) {
 #pragma unroll
@@ -1074,7 +1047,7 @@ __global__ __launch_bounds__(BK_NT) void fcseries_kernel(FcSeriesArgs a) {
     P.tmp[i] = (k < DD && b0 + c < B) ? x[(b0 + c) * DD + k] : 0.f;
   }
   Derivs<NH, BK_FCB> D;
-  mlp_pass<BK_FCB, false, ACT, NH, false, SV_SAVE>(a.f[net], nullptr, P, nullptr, &D);
+  mlp_pass<DD, BK_FCB, false, ACT, NH, false, SV_SAVE>(a.f[net], nullptr, P, nullptr, &D);
   float ev[DD];
   const bool mine = tid < BK_S && b0 + tid < B;
 #pragma unroll
@@ -1085,7 +1058,7 @@ __global__ __launch_bounds__(BK_NT) void fcseries_kernel(FcSeriesArgs a) {
   }
   float acc = 0.f;
   for (int k = 0; k < a.n_terms; ++k) {
-    mlp_pass<BK_FCB, false, ACT, NH, false, SV_VJP>(a.t[net], nullptr, P, nullptr, &D);
+    mlp_pass<DD, BK_FCB, false, ACT, NH, false, SV_VJP>(a.t[net], nullptr, P, nullptr, &D);
     if (tid < BK_S) {      // rows >= DD of the VJP are zero (the transposed output planes' padding rows)
       double tr = 0.0;
 #pragma unroll
@@ -1105,6 +1078,7 @@ int fcseries_supported(const FcSeriesArgs& a) {
     if (!a.x[i] || !a.eps[i] || !a.out[i]) return 0;
     for (int l = 0; l < a.nl; ++l)
       if (!a.f[i].L[l].Ah || !a.f[i].L[l].Aexp || !a.t[i].L[l].Ah || !a.t[i].L[l].Aexp) return 0;
+    if (!a.f[i].L[0].A || !a.t[i].L[0].A) return 0;             // the input layers' fp32 rows
   }
   return 1;
 }

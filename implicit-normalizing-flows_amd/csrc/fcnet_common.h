@@ -177,6 +177,34 @@ __device__ __forceinline__ float logdet_lu(F J) {
   return sign > 0 ? logabs : (sign == 0 ? -INFINITY : NAN);
 }
 
+// The input layer of the f16x3 fc kernels (fcnet_h3.hip, fcblock.hip) in exact fp32 on the VALU.  Its K is d and its
+// operand is the iterate itself, whose entries may span any range within one sample (a diverging Broyden step leaves
+// 1e-9 beside 0.6, the reference's prot_break fixture): the scaled fp16 split's error is relative to the column's max,
+// which drops the small entries, while a fmaf chain's error is elementwise.  The K = d contraction is ~1 % of a pass's
+// flops.  fc_in_weights: rows row0 + r (r < 4) of an operand with row stride lda, k < d (N: d's compile-time bound);
+// fc_in_col: out[r] = sum_k w[r][k] x[k * xs], a fmaf chain in k order from 0.
+template <int N>
+__device__ __forceinline__ void fc_in_weights(const float* A, int lda, int d, int row0, float (&w)[4][N]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[r][k] = k < d ? A[(long)(row0 + r) * lda + k] : 0.f;
+}
+template <int N>
+__device__ __forceinline__ void fc_in_col(const float (&w)[4][N], const float* x, int xs, int d, float (&out)[4]) {
+  float xv[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) xv[k] = k < d ? x[k * xs] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (k < d) acc = __builtin_fmaf(w[r][k], xv[k], acc);
+    out[r] = acc;
+  }
+}
+
 // Fixed power-of-two scales of the f16x3 fc kernels for Sin nets (fcnet_h3.hip explains the bounds): the forward /
 // primal hidden values (|v| <= 1 / (2 pi)) and the forward-mode tangents (|t| <= 1 where every layer's coeff <= 1)
 constexpr int FC_SFIX = 17;

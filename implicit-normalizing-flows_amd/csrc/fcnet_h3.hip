@@ -9,7 +9,8 @@
 // the producing epilogue: unscale the accumulator exactly (ldexp), bias, activation (JAC: tangents times act'), the
 // column max across the 4 lane groups (shuffles) and the 8 waves (LDS), split, write.  Three products hh + hl + lh per
 // fp32 product, fp32 accumulation: the error bound of common.h (relative to each column's and matrix's max), as on the
-// conv path.  The input rows (x, the tangent unit vectors) are split the same way (one scale per column).
+// conv path.  The input layer (K = d: x, the tangent unit vectors) is contracted in exact fp32 on the VALU instead
+// (fcnet_common.h fc_in_col): the iterate's entries may span any range within one column.
 //
 // Geometry: 8 waves, wave w owns hidden rows [16 w, 16 w + 16); 16-column blocks (FWD 3 = 48 samples, JAC d + 1 for
 // 16 samples); the d-row output layer (16 padded rows) is one row tile, column block w on wave w.  K steps of 32: the
@@ -130,28 +131,12 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
     }
     if (br_on && tid < S) broyden_update_fc<DD>(a.br, b0 + tid, d, tmp + tid, NC, e1, e2);
   }
-  // the input layer's weights (one k step), requested before the barriers
+  // the input layer's fp32 weights (exact VALU contraction, fc_in_col), requested before the barrier
   const int nl = a.nl;
-  u32x4 w0[1][2];
-  ldw_h3<1>(a.L[0].Ah, 1, w, lane, w0);
-  __syncthreads();
-  // input planes: per column, its scale and the split of rows [0, 32) (rows >= 16 are the K padding)
-  for (int c = tid; c < NC; c += H3_NT) {
-    float m = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) m = fmaxf(m, fabsf(tmp[k * NC + c]));
-    const int e = h3_scale_exp(m);
-    const float Sc = __builtin_amdgcn_ldexpf(1.f, e);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const float v = k < 16 ? tmp[k * NC + c] : 0.f;
-      const _Float16 h = (_Float16)(v * Sc);
-      const _Float16 l = (_Float16)__builtin_fmaf(v, Sc, -(float)h);
-      pl[0][0][c * H3_LD + k] = __builtin_bit_cast(uint16_t, h);
-      pl[0][1][c * H3_LD + k] = __builtin_bit_cast(uint16_t, l);
-    }
-    sx[c] = e;
-  }
+  constexpr int NI = JAC ? NCB - 1 : (DD ? DD : FC_DMAX);
+  float wi[4][NI];
+  fc_in_weights<NI>(a.L[0].A, a.L[0].Kpad, d, 16 * w + 4 * g, wi);
+  u32x4 w0[1][2];                                  // (unused: layer 0 reads the fp32 input rows)
   __syncthreads();
 
   // ---- the 128-row layers (the input layer with one k step, the hidden ones with four)
@@ -163,26 +148,32 @@ __device__ __forceinline__ void fcnet_h3_body(const FcArgs& a, long bid) {
     float bias[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[r] = L.b[16 * w + 4 * g + r];
-    f32x4 acc[NCB];
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const int col = cb * 16 + li;
-        const u32x4 xh = *reinterpret_cast<const u32x4*>(inh + col * H3_LD + ks * 32 + 8 * g);
-        const u32x4 xl = *reinterpret_cast<const u32x4*>(inl + col * H3_LD + ks * 32 + 8 * g);
-        acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
-      }
-    const int sw = ldc(L.Aexp);
     const float sp = (ACT == ACT_SWISH) ? softplus_f(ldc(L.beta)) : 0.f;
     float v[NCB][4];
+    if constexpr (NKS == 1) {
+      // the input layer: exact fp32 from the fp32 input rows (fc_in_col)
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const int e = -(sw + ((FIXS && l > 0) ? SFIX : sx[cb * 16 + li]));
+      for (int cb = 0; cb < NCB; ++cb) fc_in_col<NI>(wi, tmp + cb * 16 + li, NC, d, v[cb]);
+    } else {
+      f32x4 acc[NCB];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
+      for (int cb = 0; cb < NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int col = cb * 16 + li;
+          const u32x4 xh = *reinterpret_cast<const u32x4*>(inh + col * H3_LD + ks * 32 + 8 * g);
+          const u32x4 xl = *reinterpret_cast<const u32x4*>(inl + col * H3_LD + ks * 32 + 8 * g);
+          acc[cb] = mfma3(wr[ks], xh, xl, acc[cb]);
+        }
+      const int sw = ldc(L.Aexp);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int e = -(sw + (FIXS ? SFIX : sx[cb * 16 + li]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[cb][r] = __builtin_amdgcn_ldexpf(acc[cb][r], e);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

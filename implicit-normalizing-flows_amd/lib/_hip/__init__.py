@@ -6,6 +6,7 @@ parameter tensor changes (tracked through torch's version counters / storage poi
 Nothing here computes: every numerical op of the hot path runs in libinflow.so, and a missing
 library raises instead of falling back to PyTorch.
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -86,6 +87,7 @@ _lock = threading.Lock()
 _P = ctypes.c_void_p
 _SIGS = {
     'inf_version': (ctypes.c_int, []),
+    'inf_shutdown': (ctypes.c_int, []),
     'inf_status_string': (ctypes.c_char_p, [ctypes.c_int]),
     'inf_last_hip_error': (ctypes.c_int, []),
     'inf_net_create': (ctypes.c_int, [ctypes.POINTER(NetDesc), ctypes.POINTER(_P)]),
@@ -170,7 +172,15 @@ def load(path=LIB_PATH):
                 fn.restype = res
                 fn.argtypes = args
             _lib = lib
+            atexit.register(_shutdown)
         return _lib
+
+
+def _shutdown():
+    """atexit: release the engine's host resources (pinned readback slots, events, side streams) before the HIP
+    runtime's own exit-time teardown (inf_shutdown).  Only when this process used the GPU."""
+    if _lib is not None and torch.cuda.is_initialized():
+        _lib.inf_shutdown()
 
 
 def check(status, what):

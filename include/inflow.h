@@ -81,6 +81,10 @@ typedef struct InfBroydenStats {  /* mirrors the dict returned by broyden() (bro
 
 /* ---- library ------------------------------------------------------------------------------ */
 int inf_version(void);
+/* Releases the calling thread's engine-held host resources (pinned readback slots, events, side streams, profiling
+ * events) after waiting for the device.  Call before process exit: lib/_hip registers it with atexit, so it runs before
+ * the HIP runtime's own teardown.  Idempotent; nets stay valid and later calls re-create what they need. */
+int inf_shutdown(void);
 const char* inf_status_string(int status);
 int inf_last_hip_error(void);
 
@@ -233,7 +237,8 @@ int inf_imblock_eval_exact(InfNet* net_x, InfNet* net_z, const float* x, float* 
  * host round trip between blocks beyond a block's own.  thresholds / eps: per block; stats: n_blocks entries or NULL.
  * With f16x3 nets on the launch path, block i's z-branch log-det launch also evaluates block i+1's x-branch (log-det
  * and x_embed at the same z): one grid for the two Jacobians; results identical to the blocks called one by one.
- * INF_ERR_UNSUPPORTED (before any launch) when a block is not on the fused fc path.
+ * INF_ERR_UNSUPPORTED (before any launch) when a block is not on the fused fc path; INF_ERR_INVALID when x == z or
+ * logp_in == logp_out (the step is not in place here: a re-queued z-branch launch would apply it twice).
  * ws >= inf_flow_chain_workspace_bytes(net_z, n_blocks, batch, thresholds). */
 size_t inf_flow_chain_workspace_bytes(InfNet* const* net_z, int n_blocks, int batch, const int* thresholds);
 int inf_flow_eval_exact_chain(InfNet* const* net_x, InfNet* const* net_z, int n_blocks, const float* x, float* z,

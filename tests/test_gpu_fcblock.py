@@ -84,6 +84,32 @@ def test_block_kernel_matches_launch_path(arch, B, convergence):
     assert err <= 2e-5 * max(1.0, per[2].abs().max().item()), err
 
 
+@pytest.mark.parametrize('convergence', ['global', 'per_sample'])
+def test_block_kernel_wide_grid_matches_launch_path(convergence):
+    """B = 13 000 on the toy net: 271 workgroups of 48 samples, more than the 256 whose partials one 512-granule read of
+    the global rule's exchange covers (fcblock.hip gather_total reads the granules 512 at a time).  Per sample the block
+    kernel runs (no exchange); under the global rule it runs when the grid is co-resident and otherwise the cooperative
+    launch is refused and the launch path takes the block.  Either way: the launch path's step counts, nats within 1e-5,
+    z within 2e-5."""
+    arch, B = syn.TOY, 13000
+    x = syn.tabular_batch(B, arch['d'], seed=29).to(DEV)
+    m, _ = _model(arch, B)
+    blk = _eval(m, x, 2, convergence)
+    per = _eval(m, x, 0, convergence)
+    if convergence == 'per_sample':
+        assert TAG_BLOCK in blk[4], sorted(blk[4])
+    for a, b in zip(blk[3], per[3]):
+        assert a['prot_break'] == b['prot_break'] == 0
+        if convergence == 'global':
+            assert (a['nstep'], a['lowest_step']) == (b['nstep'], b['lowest_step']), (a, b)
+        else:
+            na, nb = np.array(a['sample_nstep']), np.array(b['sample_nstep'])
+            assert np.abs(na - nb).max() <= 1 and (na != nb).mean() <= 0.01
+    assert abs(blk[0] - per[0]) <= 1e-5, (blk[0], per[0])
+    err = (blk[2] - per[2]).abs().max().item()
+    assert err <= 2e-5 * max(1.0, per[2].abs().max().item()), err
+
+
 def _prot_break_deep_block():
     p = syn.PROT_BREAK_DEEP
     lin = lambda a, b: get_linear(a, b, coeff=p['coeff'], n_iterations=None, atol=1e-3, rtol=1e-3, domain=2,
@@ -132,21 +158,31 @@ def _load_prot_break_deep(golden_dir):
     return g, x
 
 
+@pytest.mark.parametrize('arith,fc_block', [('f32', 0), ('f16x3', 0), ('f16x3', 2)],
+                         ids=['f32_launch', 'f16x3_launch', 'f16x3_block'])
 @pytest.mark.parametrize('convergence', ['global', 'per_sample'])
-def test_protective_break_fused_fc_launch_path_matches_reference(golden_dir, convergence, monkeypatch):
-    """prot_break_deep_b6 (the reference on PROT_BREAK_DEEP, the POWER nets' shape) on the fused fc launch path with
-    exact fp32 MFMA (fcnet.hip, INFLOW_MFMA=f32): the protective-break branch of inf_imblock_eval_exact (Banach fallback
-    from the solve's buffers, the z recompute, the z-branch Jacobian on the recomputed z).  Global rule -> the batch
-    breaks at step 1 and takes the fixed point; per-sample rule -> the coupled samples break, the samples with x0 == 0
-    converge in Broyden.  prot_break, step counts and the fixed-point iteration count exact; z within 2e-5 of its max,
-    per-sample log p within 2e-3 nats, nats within 1e-5.  (The scaled fp16 split cannot carry this fixture: after the
-    first step an iterate holds 1e-9 and 0.6 in one column, and the split's error is relative to the column's max.)"""
+def test_protective_break_fused_fc_launch_path_matches_reference(golden_dir, convergence, arith, fc_block, monkeypatch):
+    """prot_break_deep_b6 (the reference on PROT_BREAK_DEEP, the POWER nets' shape) on the fused fc paths: the exact
+    fp32 MFMA launch path (fcnet.hip, INFLOW_MFMA=f32), the default f16x3 launch path (fcnet_h3.hip) and the default
+    block kernel (fcblock.hip).  The protective-break branch of inf_imblock_eval_exact (Banach fallback from the solve's
+    buffers, the z recompute, the z-branch Jacobian on the recomputed z).  Global rule -> the batch breaks at step 1 and
+    takes the fixed point; per-sample rule -> the coupled samples break, the samples with x0 == 0 converge in Broyden.
+    prot_break, step counts and the fixed-point iteration count exact; z within 2e-5 of its max, per-sample log p within
+    2e-3 nats, nats within 1e-5.  After the first Broyden step an iterate holds 1e-9 and 0.6 in one column: the f16x3
+    kernels carry it because their input layer (K = d, the iterate itself) is contracted in exact fp32 (fcnet_h3.hip,
+    fcblock.hip), so the split's column-relative error never touches the iterate's small entries."""
     g, x = _load_prot_break_deep(golden_dir)
     tag = 'g' if convergence == 'global' else 'ps'
-    monkeypatch.setenv('INFLOW_MFMA', 'f32')
-    z, lp, st, tags, nets = _run_prot_break_deep(x, convergence, 0)
-    assert all(n.lib.inf_net_get_mfma(n.handle) == 0 for n in nets)
-    assert 601 in tags and TAG_BLOCK not in tags, sorted(tags)
+    if arith == 'f32':
+        monkeypatch.setenv('INFLOW_MFMA', 'f32')
+    else:
+        monkeypatch.delenv('INFLOW_MFMA', raising=False)
+    z, lp, st, tags, nets = _run_prot_break_deep(x, convergence, fc_block)
+    assert all(n.lib.inf_net_get_mfma(n.handle) == (0 if arith == 'f32' else 2) for n in nets)
+    if fc_block:
+        assert TAG_BLOCK in tags, sorted(tags)
+    else:
+        assert 601 in tags and TAG_BLOCK not in tags, sorted(tags)
     assert st['prot_break'], st
     fp_ref = g[tag + '_fixed_point_iters']
     assert st['fixed_point_iters'] == int(fp_ref.max()), (st['fixed_point_iters'], fp_ref)

@@ -1,6 +1,6 @@
 """Mean SQ counters per dispatch of the VJP kernels in rocprofv3 --pmc CSVs (tools/r5_pmc_sq_k.sh), with the derived
 fractions: MFMA-busy share of the SIMD cycles, wait / active shares of the wave cycles, mean waves per SIMD.
-    python tools/sq_summary.py gpurun_out/r5_sq_k3_s0"""
+    python tools/sq_summary.py gpurun_out/r5_sq_k3_s0 [kernel-name substring, e.g. fcblock_kernel]"""
 import collections
 import csv
 import glob
@@ -8,11 +8,12 @@ import os
 import sys
 
 d = sys.argv[1]
+pat = sys.argv[2] if len(sys.argv) > 2 else None
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        if ('net313k_kernel<2' in k or 'net313p_kernel' in k):
+        if (pat in k) if pat else ('net313k_kernel<2' in k or 'net313p_kernel' in k):
             agg[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k, c in agg.items():
     m = {n: sum(v) / len(v) for n, v in c.items()}
