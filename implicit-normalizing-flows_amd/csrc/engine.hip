@@ -123,6 +123,7 @@ struct InfNet {
   int k128 = 1;            // INF_OPT_FUSED_K128
   int eval_overlap = 1;    // INF_OPT_EVAL_OVERLAP (read on net_x of inf_imblock_eval)
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
+  int line_search = 0;                 // INF_OPT_LINE_SEARCH (read on the solved net)
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
   int fc_block = 1;        // INF_OPT_FC_BLOCK (read on net_z of inf_imblock_eval_exact)
   int fc_series = 1;       // INF_OPT_FC_SERIES (read on the first net of inf_logdet_series[_pair])
@@ -665,6 +666,7 @@ static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vecto
     if (stats.sample_prot_break) stats.sample_prot_break[b] = pb;
   }
   stats.nstep = nmax;
+  stats.tnstep = nmax;
   stats.lowest_step = lmax;
   stats.prot_break = prot;
   stats.diff = sqrt(d2);
@@ -924,6 +926,225 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
     bf.fspec = fr[1];
   }
   stats.nstep = nstep;
+  stats.tnstep = nstep;
+  stats.lowest_step = lowest_step;
+  stats.diff = lowest;
+  return INF_OK;
+}
+
+// _safe_norm(g)**2 (broyden.py:18-21,81) from the per-sample sums of squares: the fp32 norm squared in fp32, inf when
+// any entry is not finite
+static float ls_phi(const std::vector<double>& ss) {
+  const double t = total(ss);
+  if (!std::isfinite(t)) return INFINITY;
+  const float n = (float)sqrt(t);
+  return n * n;
+}
+
+// broyden.py:123-193 with line_search(on=True) (:66-99) and scalar_search_armijo (:24-63; c1 = 1e-4, alpha0 = 1,
+// amin = 1e-2, derphi0 = -phi0), the global rule.  Each step: the trial point x0 + s update (launch_line_step; s = 1 is
+// the update launch's own x + update), its residual and norm read back (one host round trip per evaluation: the step
+// size decides the next point, so nothing is speculated), the quadratic then cubic backtracking in fp32 as the
+// reference's 0-d fp32 tensors compute it, the last evaluation reused when the accepted step is the stored one (:77-78,
+// 95-96).  A failed search takes the full step with ite = 0 and evaluates it again (:90-98).  stats.tnstep counts
+// nstep + the accepted searches' extra iterations (:156).  Result (lowest iterate) in bf.lowest, its f in bf.flow.
+int broyden_core_ls(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
+                    std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f) {
+#pragma clang fp contract(off)
+  const size_t E = (size_t)B * f->d;
+  const long cs = (long)E;
+  const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
+  {
+    int *a = stats.sample_nstep, *b = stats.sample_lowest_step, *c = stats.sample_prot_break;
+    memset(&stats, 0, sizeof(stats));
+    stats.sample_nstep = a;
+    stats.sample_lowest_step = b;
+    stats.sample_prot_break = c;
+  }
+  const double eps = eps_in * sqrt((double)E);                       // broyden.py:131
+  stats.eps = eps;
+  stats.convergence = INF_CONV_GLOBAL;
+  float* xpool[3] = {bf.xa, bf.xb, bf.lowest};
+  float* fpool[3] = {bf.fcur, bf.flow, bf.fspec};
+  auto pick = [](float* const* pool, const float* a, const float* b) {
+    for (int i = 0; i < 3; ++i)
+      if (pool[i] != a && pool[i] != b) return pool[i];
+    return pool[0];
+  };
+  float* x = xpool[0];
+  float* fx = fpool[0];
+  float *gx = bf.ga, *gt = bf.gb;
+  std::vector<double> ss(B), ss_t(B);
+  INF_HIP(hipMemsetAsync(x, 0, sizeof(float) * E, s));
+  bf.fcur = fx;
+  INF_TRY(resid(x, gx, nullptr, nullptr));
+  INF_TRY(read_sumsq(f, B, bf, ss, s));
+  const double init = sqrt(total(ss));
+  double obj = init, lowest = init;
+  lowest_ss = ss;
+  float* low = x;
+  float* flow = keep_f ? fx : nullptr;
+  int nstep = 0, tnstep = 0, lowest_step = 0;
+  std::vector<double> trace{init};
+  INF_TRY(launch_neg(gx, bf.upd, (long)E, s));                      // update = -gx (:144)
+  float* xt = pick(xpool, low, x);
+  INF_TRY(launch_axpy_step(x, bf.upd, xt, bf.dx, (long)E, s));       // the s = 1 trial point
+  bool xt_full = true;                                               // xt holds x + 1 * update
+  auto update_args = [&](int step, float* xfrom, float* gfrom, float* xto) {
+    BroydenArgs ba;
+    memset(&ba, 0, sizeof(ba));
+    ba.batch = B;
+    ba.d = f->d;
+    ba.T = T;
+    ba.sb = sb;
+    ba.si = si;
+    ba.cs = cs;
+    ba.U = bf.U;
+    ba.VT = bf.VT;
+    ba.dx = bf.dx;
+    ba.dg = bf.dg;
+    ba.gx = gfrom;
+    ba.x = xfrom;
+    ba.xnew = xto;
+    ba.dxnew = bf.dx;
+    ba.upd = bf.upd;
+    ba.part = bf.bpart;
+    ba.m = (step - 1) % T;
+    ba.ncols = std::min(step, T);
+    return ba;
+  };
+  while (obj >= eps && nstep < T) {                                  // :153
+    // ---- line_search(update, x, gx, g, on=True): the stored evaluation starts as (s = 0, phi0, g0)
+    const float phi0 = ls_phi(ss), der = -phi0;
+    float st_s = 0.f, st_phi = phi0;
+    bool st_init = true;                                             // the stored evaluation is (x, gx) itself
+    float* ft = nullptr;
+    auto phi = [&](float sv, float& out) -> int {                   // :76-86
+      if (sv == st_s) {
+        out = st_phi;
+        return INF_OK;
+      }
+      if (!(sv == 1.f && xt_full)) INF_TRY(launch_line_step(x, bf.upd, sv, xt, bf.dx, (long)E, s));
+      xt_full = sv == 1.f;
+      ft = pick(fpool, flow, fx);
+      bf.fcur = ft;
+      INF_TRY(resid(xt, gt, bf.dg, gx));                             // g, f and dg = g - g0 of the trial point
+      INF_TRY(read_sumsq(f, B, bf, ss_t, s));
+      out = ls_phi(ss_t);
+      st_s = sv;
+      st_phi = out;
+      st_init = false;
+      return INF_OK;
+    };
+    const float c1 = 1e-4f, amin = 1e-2f;
+    float acc = 1.f;
+    bool found = false;
+    int ite = 0;
+    float pa0;
+    INF_TRY(phi(1.f, pa0));                                          // scalar_search_armijo (:24-63)
+    if (pa0 <= phi0 + c1 * der) {
+      found = true;
+    } else {
+      float a0 = 1.f;
+      float a1 = -der * 1.f / 2.f / (pa0 - phi0 - der * a0);
+      float pa1;
+      INF_TRY(phi(a1, pa1));
+      while (a1 > amin) {
+        const float fac = a0 * a0 * (a1 * a1) * (a1 - a0);
+        const float r1 = pa1 - phi0 - der * a1, r0 = pa0 - phi0 - der * a0;
+        float a = a0 * a0 * r1 - a1 * a1 * r0;
+        a = a / fac;
+        float b = -(a0 * a0 * a0) * r1 + a1 * a1 * a1 * r0;
+        b = b / fac;
+        float a2 = (-b + sqrtf(fabsf(b * b - 3.f * a * der))) / (3.f * a);
+        float pa2;
+        INF_TRY(phi(a2, pa2));
+        ite += 1;
+        if (pa2 <= phi0 + c1 * a2 * der) {
+          acc = a2;
+          found = true;
+          break;
+        }
+        if ((a1 - a2) > a1 / 2.f || (1.f - a2 / a1) < 0.96f) a2 = a1 / 2.f;
+        a0 = a1;
+        a1 = a2;
+        pa0 = pa1;
+        pa1 = pa2;
+      }
+    }
+    if (!found) {                                                    // :90-92
+      acc = 1.f;
+      ite = 0;
+    }
+    if (acc != st_s) {                                               // :94-98 (a fresh evaluation at the step)
+      st_s = acc + 1.f;                                              // (anything else: phi evaluates)
+      float unused;
+      INF_TRY(phi(acc, unused));
+    } else if (st_init) {                                            // the accepted step is 0: x0 and g0 themselves
+      INF_TRY(launch_line_step(x, bf.upd, 0.f, xt, bf.dx, (long)E, s));
+      ft = pick(fpool, flow, fx);
+      INF_HIP(hipMemcpyAsync(gt, gx, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+      INF_HIP(hipMemsetAsync(bf.dg, 0, sizeof(float) * E, s));
+      if (keep_f) INF_HIP(hipMemcpyAsync(ft, fx, sizeof(float) * E, hipMemcpyDeviceToDevice, s));
+      ss_t = ss;
+      xt_full = false;
+    }
+    // ---- the step is taken: x_est, g(x_est), delta_x (bf.dx), delta_g (bf.dg)
+    x = xt;
+    std::swap(gx, gt);
+    fx = ft;
+    ss = ss_t;
+    nstep += 1;
+    tnstep += ite + 1;                                               // :155-156
+    obj = sqrt(total(ss));
+    trace.push_back(obj);
+    if (obj < lowest) {                                              // :159-162
+      low = x;
+      if (keep_f) flow = fx;
+      lowest = obj;
+      lowest_step = nstep;
+      lowest_ss = ss;
+    }
+    if (obj < eps) break;                                            // :163-164
+    if (obj < 3 * eps && nstep == T) {                               // :165-168
+      const size_t k0 = trace.size() > (size_t)T ? trace.size() - T : 0;
+      double mx = trace[k0], mn = trace[k0];
+      for (size_t k = k0; k < trace.size(); ++k) {
+        mx = std::max(mx, trace[k]);
+        mn = std::min(mn, trace[k]);
+      }
+      if (mx / mn < 1.3) break;
+    }
+    if (obj > init * 1e6) {                                          // :169-172
+      stats.prot_break = 1;
+      break;
+    }
+    // the rank-1 update and update = -matvec(...) (:174-181); its x + update is the next search's s = 1 point
+    xt = pick(xpool, low, x);
+    INF_TRY(launch_broyden_update(update_args(nstep, x, gx, xt), s));
+    xt_full = true;
+  }
+  stats.n_trace = (int)std::min<size_t>(trace.size(), 64);
+  for (int k = 0; k < stats.n_trace; ++k) stats.trace[k] = trace[k];
+  {
+    float* rest[2];
+    int k = 0;
+    for (float* p : xpool)
+      if (p != low && k < 2) rest[k++] = p;
+    bf.lowest = low;
+    bf.xa = rest[0];
+    bf.xb = rest[1];
+    float* fr[2];
+    k = 0;
+    const float* fl = flow ? flow : fpool[1];
+    for (float* p : fpool)
+      if (p != fl && k < 2) fr[k++] = p;
+    bf.flow = const_cast<float*>(fl);
+    bf.fcur = fr[0];
+    bf.fspec = fr[1];
+  }
+  stats.nstep = nstep;
+  stats.tnstep = tnstep;
   stats.lowest_step = lowest_step;
   stats.diff = lowest;
   return INF_OK;
@@ -1058,8 +1279,14 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, bf.stop_ev, &bf.stop_bound, upd, x1, dx,
                                    B, f->d, s);
   };
-  INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
-                       f->fc ? &start : nullptr, tail));
+  if (f->line_search) {
+    // line_search(on=True) (broyden.py:66-99): the global rule only (a per-sample step size is not the reference's)
+    if (f->convergence != INF_CONV_GLOBAL) return INF_ERR_UNSUPPORTED;
+    INF_TRY(broyden_core_ls(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
+  } else {
+    INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
+                         f->fc ? &start : nullptr, tail));
+  }
   if (diff_detail) {
     std::vector<float> dd(B);
     for (int b = 0; b < B; ++b) dd[b] = (float)sqrt(lowest_ss[b]);
@@ -1093,7 +1320,8 @@ static thread_local size_t g_bk_host_cap = 0;
 static thread_local hipEvent_t g_bk_ev = nullptr;
 int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logdet_x, float* logdet_z, int B, int T,
                   double eps_in, InfBroydenStats* stats, Bufs& bf, hipStream_t s) {
-  if (nx->mfma_mode != INF_MFMA_F16X3 || nz->mfma_mode != INF_MFMA_F16X3 || !bf.bk_sync) return INF_ERR_UNSUPPORTED;
+  if (nx->mfma_mode != INF_MFMA_F16X3 || nz->mfma_mode != INF_MFMA_F16X3 || !bf.bk_sync || nz->line_search)
+    return INF_ERR_UNSUPPORTED;
   FcBlockArgs a;
   memset(&a, 0, sizeof(a));
   a.nx = fc_args(nx, nullptr, B);
@@ -1179,6 +1407,7 @@ int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logde
     st.diff = sqrt(d2);
     st.eps = a.eps_ps;
   }
+  st.tnstep = st.nstep;
   if (st.prot_break) {
     // banach_find_root (implicit_block.py:57-65,74-75) from z0 = x, as broyden_solve does, on the buffers the kernel
     // left: x_embed, f_x(x), x and the lowest iterates (per-sample rule: only the samples whose own solve broke)
@@ -2603,6 +2832,12 @@ int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, co
   return launch_broyden_update(ba, (hipStream_t)stream);
 }
 
+int inf_broyden_line_step(const float* x0, const float* update, float step, float* x_est, float* dx, size_t n,
+                          void* stream) {
+  if (!x0 || !update || !x_est || !dx || n == 0) return INF_ERR_INVALID;
+  return launch_line_step(x0, update, step, x_est, dx, (long)n, (hipStream_t)stream);
+}
+
 // ---- teardown ---------------------------------------------------------------------------------
 // The calling thread's engine-held host resources: the pinned readback slots and their events, the block kernel's
 // statistics buffer and event, the side streams and their fork / join events, the profiling events.  They were kept
@@ -2853,6 +3088,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_FUSED_K128: slot = &n->k128; hi = 3; break;
     case INF_OPT_EVAL_OVERLAP: slot = &n->eval_overlap; hi = 1; break;
     case INF_OPT_CONVERGENCE: slot = &n->convergence; hi = 1; break;
+    case INF_OPT_LINE_SEARCH: slot = &n->line_search; hi = 1; break;
     case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;
     case INF_OPT_FC_BLOCK: slot = &n->fc_block; hi = 2; break;
     case INF_OPT_FC_SERIES: slot = &n->fc_series; hi = 1; break;
@@ -2872,6 +3108,7 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_FUSED_K128: return n->k128;
     case INF_OPT_EVAL_OVERLAP: return n->eval_overlap;
     case INF_OPT_CONVERGENCE: return n->convergence;
+    case INF_OPT_LINE_SEARCH: return n->line_search;
     case INF_OPT_K128_EXACT_SCALE: return n->exact_scale;
     case INF_OPT_FC_BLOCK: return n->fc_block;
     case INF_OPT_FC_SERIES: return n->fc_series;

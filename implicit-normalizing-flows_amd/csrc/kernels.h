@@ -73,6 +73,8 @@ int launch_fc_out(const OutArgs& a, int batch, hipStream_t s);
 int launch_transpose(const float* x, float* y, int rows, int cols, hipStream_t s);  // y[c][r] = x[r][c]
 int launch_axpy_step(const float* x, const float* upd, float* xnew, float* dx, long n, hipStream_t s);
 int launch_neg(const float* x, float* y, long n, hipStream_t s);
+// x_est = x0 + sc * upd, dx = x_est - x0 (the line search's trial point; product and sum rounded separately)
+int launch_line_step(const float* x, const float* upd, float sc, float* xnew, float* dx, long n, hipStream_t s);
 // stop_ev (optional): an event the launch itself completes (hipExtLaunchKernel; not while profiling), *stop_bound set
 int launch_reduce_partials(const double* partial, int batch, int nchunk, double* out, hipStream_t s,
                            hipEvent_t stop_ev = nullptr, bool* stop_bound = nullptr);

@@ -317,6 +317,20 @@ int launch_axpy_step(const float* x, const float* upd, float* xnew, float* dx, l
   INF_PROF_LAUNCH(s, 703, 16.0 * n, axpy_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, xnew, dx, n);
   return INF_OK;
 }
+// line_search(on=True)'s trial point x_est = x0 + s * update and delta_x = x_est - x0 (broyden.py:79,94,99): the product
+// and the sum rounded separately, as the reference's two tensor ops do (no contraction into an fma)
+__global__ void line_step_kernel(const float* x, const float* upd, float sc, float* xnew, float* dx, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x0 = x[i];
+  const float xe = __fadd_rn(x0, __fmul_rn(sc, upd[i]));
+  xnew[i] = xe;
+  dx[i] = __fsub_rn(xe, x0);
+}
+int launch_line_step(const float* x, const float* upd, float sc, float* xnew, float* dx, long n, hipStream_t s) {
+  INF_PROF_LAUNCH(s, 705, 16.0 * n, line_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, sc, xnew, dx, n);
+  return INF_OK;
+}
 __global__ void neg_kernel(const float* x, float* y, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) y[i] = -x[i];

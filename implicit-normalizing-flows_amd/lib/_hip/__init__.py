@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
 INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE, INF_OPT_K128_EXACT_SCALE = 1, 2, 3, 4   # InfNetOption
-INF_OPT_FC_BLOCK, INF_OPT_FC_SERIES = 5, 6
+INF_OPT_FC_BLOCK, INF_OPT_FC_SERIES, INF_OPT_LINE_SEARCH = 5, 6, 7
 INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
 CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 
@@ -52,7 +52,7 @@ class BroydenStats(ctypes.Structure):
                 ('n_trace', ctypes.c_int), ('trace', ctypes.c_double * 64), ('diff', ctypes.c_double),
                 ('eps', ctypes.c_double), ('fixed_point_iters', ctypes.c_int), ('convergence', ctypes.c_int),
                 ('sample_nstep', ctypes.POINTER(ctypes.c_int)), ('sample_lowest_step', ctypes.POINTER(ctypes.c_int)),
-                ('sample_prot_break', ctypes.POINTER(ctypes.c_int))]
+                ('sample_prot_break', ctypes.POINTER(ctypes.c_int)), ('tnstep', ctypes.c_int)]
 
     def want_samples(self, batch):
         """Per-sample outcome arrays (INF_CONV_PER_SAMPLE): host buffers the engine fills."""
@@ -62,7 +62,7 @@ class BroydenStats(ctypes.Structure):
         return self
 
     def as_dict(self, threshold):
-        d = {'nstep': self.nstep, 'tnstep': self.nstep, 'lowest_step': self.lowest_step,
+        d = {'nstep': self.nstep, 'tnstep': self.tnstep, 'lowest_step': self.lowest_step,
              'diff': self.diff, 'prot_break': bool(self.prot_break),
              'trace': [self.trace[i] for i in range(self.n_trace)], 'eps': self.eps,
              'threshold': threshold, 'fixed_point_iters': self.fixed_point_iters,
@@ -118,6 +118,7 @@ _SIGS = {
     'inf_broyden_workspace_bytes': (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     'inf_broyden_update': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, _P, ctypes.c_size_t, _P]),
+    'inf_broyden_line_step': (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, ctypes.c_size_t, _P]),
     'inf_logdet_series': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P,
                                          ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_logdet_series_pair': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int,

@@ -211,8 +211,10 @@ class RootFind:
     """RootFind.apply(nnet_z, nnet_x, z0, x, method, eps, threshold) (implicit_block.py:51-100): the root z of
     z + nnet_z(z) = x + nnet_x(x), by 'broyden' (from 0, Banach fallback on prot_break; inf_root_find) or 'banach'
     (find_fixed_point from z0, :57-65; inf_banach_find_root).  No gradient (the reference's backward asserts).
-    The solve's statistics are left in RootFind.last (dict)."""
+    The solve's statistics are left in RootFind.last (dict).  RootFind.line_search = True runs the Broyden solve with
+    line_search(on=True) (broyden.py:24-99; INF_OPT_LINE_SEARCH on nnet_z's engine net)."""
     last = None
+    line_search = False
 
     @staticmethod
     def apply(nnet_z, nnet_x, z0, x, method, *args):
@@ -233,6 +235,9 @@ class RootFind:
             nets.append(n)
         nf, ne = nets
         out = torch.empty_like(x)
+        ls = int(bool(RootFind.line_search))
+        if nf.get_option(_hip.INF_OPT_LINE_SEARCH) != ls:
+            nf.set_option(_hip.INF_OPT_LINE_SEARCH, ls)
         if method == 'broyden':
             ws = _hip.workspace(x.device, max(nf.ws_bytes(B, threshold), ne.ws_bytes(B, threshold)))
             st = _stats(B, (nf,))
@@ -400,6 +405,8 @@ class imBlock(nn.Module):
         self.register_buffer('last_secmom', torch.zeros(1))
         self.last_broyden = None
         self.convergence = None          # None: the module default (set_convergence); 'global' / 'per_sample'
+        self.line_search = False         # broyden(..., ls=True) for the root solves (INF_OPT_LINE_SEARCH; the
+                                         # reference's call sites never pass ls, broyden.py:24-99)
 
     # ---------------------------------------------------------------------------------------
     def _native(self, t):
@@ -419,6 +426,9 @@ class imBlock(nn.Module):
             n.refresh_if_needed(stream)
             if n.get_option(_hip.INF_OPT_CONVERGENCE) != conv:
                 n.set_option(_hip.INF_OPT_CONVERGENCE, conv)
+            ls = int(bool(getattr(self, 'line_search', False)))
+            if n.get_option(_hip.INF_OPT_LINE_SEARCH) != ls:
+                n.set_option(_hip.INF_OPT_LINE_SEARCH, ls)
             nets.append(n)
         return nets[0], nets[1], stream
 

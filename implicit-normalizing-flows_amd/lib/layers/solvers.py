@@ -22,16 +22,51 @@ __all__ = ['broyden', 'find_fixed_point', 'basic_logdet_estimator', 'neumann_log
 
 
 # ---------------------------------------------------------------------------------------------
-# Broyden (broyden.py:123-193), line search off
+# Broyden (broyden.py:123-193), with or without the line search (:24-99)
 # ---------------------------------------------------------------------------------------------
+def _armijo(phi, phi0):
+    """scalar_search_armijo (broyden.py:24-63) as line_search(on=True) runs it (:89): derphi0 = -phi0, c1 = 1e-4,
+    alpha0 = 1, amin = 1e-2, in the reference's 0-d fp32 tensor arithmetic (phi returns a 0-d fp32 CPU tensor, or inf).
+    Returns (the accepted step or None, the cubic iterations)."""
+    slope = -phi0
+    pa0 = phi(1)
+    if pa0 <= phi0 + 1e-4 * slope:
+        return 1, 0
+    lo = 1
+    hi = -slope * lo ** 2 / 2.0 / (pa0 - phi0 - slope * lo)       # quadratic interpolant's minimiser
+    p_hi = phi(hi)
+    it = 0
+    while hi > 1e-2:
+        e_lo, e_hi = pa0 - phi0 - slope * lo, p_hi - phi0 - slope * hi
+        den = lo ** 2 * hi ** 2 * (hi - lo)
+        c3 = (lo ** 2 * e_hi - hi ** 2 * e_lo) / den                # cubic interpolant: c3 s^3 + c2 s^2 + slope s + phi0
+        c2 = (-lo ** 3 * e_hi + hi ** 3 * e_lo) / den
+        nxt = (-c2 + torch.sqrt(torch.abs(c2 ** 2 - 3 * c3 * slope))) / (3.0 * c3)
+        p_nxt = phi(nxt)
+        it += 1
+        if p_nxt <= phi0 + 1e-4 * nxt * slope:
+            return nxt, it
+        if (hi - nxt) > hi / 2.0 or (1 - nxt / hi) < 0.96:
+            nxt = hi / 2.0
+        lo, hi, pa0, p_hi = hi, nxt, p_hi, p_nxt
+    return None, it
+
+
+def _sq_norm(v):
+    """_safe_norm(v) ** 2 (broyden.py:18-21,81): inf when an entry is not finite, else the fp32 norm squared."""
+    if not bool(torch.isfinite(v).all()):
+        return np.inf
+    return (torch.norm(v) ** 2).cpu()
+
+
 def broyden(g_, x0, threshold, eps, ls=False, name='unknown'):
     """Limited-memory good-Broyden root solve of g_(x) = 0 from x0.
 
     Same stopping rules and result dict as the reference: global Frobenius residual against
-    eps * sqrt(B*d), lowest-residual iterate returned, stall and protective breaks.
+    eps * sqrt(B*d), lowest-residual iterate returned, stall and protective breaks.  ls=True: each step's size from the
+    Armijo search of line_search(on=True) (broyden.py:66-99), its trial points x0 + s update on the engine
+    (inf_broyden_line_step) and g_ evaluated at each; tnstep counts the accepted searches' iterations (:156).
     """
-    if ls:
-        raise NotImplementedError('line search is never enabled by the reference call sites (broyden.py:88-92)')
     _hip.require_device(x0, 'broyden')
     lib = _hip.load()
     shape = x0.shape
@@ -48,6 +83,30 @@ def broyden(g_, x0, threshold, eps, ls=False, name='unknown'):
     VT = torch.zeros(T, bsz, d, device=x.device, dtype=x.dtype)
     ws = torch.empty(lib.inf_broyden_workspace_bytes(bsz, d, T), dtype=torch.uint8, device=x.device)
     stream = _hip.stream_of(x)
+
+    def trial(x_from, upd, step):
+        """x_from + step * upd and its difference from x_from (broyden.py:79,94,99)."""
+        xe, dx_ = torch.empty_like(x_from), torch.empty_like(x_from)
+        _hip.check(lib.inf_broyden_line_step(_hip.ptr(x_from), _hip.ptr(upd), float(step), _hip.ptr(xe), _hip.ptr(dx_),
+                                             x_from.numel(), stream), 'inf_broyden_line_step')
+        return xe, dx_
+
+    def search(x_from, g_from, upd):
+        """line_search(upd, x_from, g_from, g, on=True): (x_est, g(x_est), iterations)."""
+        kept = {'s': 0, 'phi': (torch.norm(g_from) ** 2).cpu(), 'g': g_from}
+
+        def phi(step):
+            if step == kept['s']:
+                return kept['phi']
+            gv = g(trial(x_from, upd, step)[0])
+            kept.update(s=step, g=gv, phi=_sq_norm(gv))
+            return kept['phi']
+        step, it = _armijo(phi, kept['phi'])
+        if step is None:                                            # the search failed: the full step (:90-92)
+            step, it = 1.0, 0
+        x_est = trial(x_from, upd, step)[0]
+        return x_est, (kept['g'] if step == kept['s'] else g(x_est)), it
+
     gx = g(x)
     update = -gx
     x_next = x + update
@@ -55,13 +114,18 @@ def broyden(g_, x0, threshold, eps, ls=False, name='unknown'):
     init = new = torch.norm(gx).item()
     trace = [init]
     lowest, lowest_x, lowest_g, lowest_step = init, x, gx, 0
-    nstep = 0
+    nstep = tnstep = 0
     prot_break = False
     while new >= eps_s and nstep < T:
-        g_next = g(x_next)
+        if ls:
+            x_next, g_next, it = search(x, gx, update)
+            dx = x_next - x
+        else:
+            g_next, it = g(x_next), 0
         dg = g_next - gx
         x, gx = x_next, g_next
         nstep += 1
+        tnstep += it + 1
         new = torch.norm(gx).item()
         trace.append(new)
         if new < lowest:
@@ -78,7 +142,7 @@ def broyden(g_, x0, threshold, eps, ls=False, name='unknown'):
                                           _hip.ptr(x), _hip.ptr(update), _hip.ptr(x_next), _hip.ptr(dx_new), bsz, d,
                                           T, nstep, _hip.ptr(ws), ws.numel(), stream), 'inf_broyden_update')
         dx = dx_new
-    return {'result': lowest_x.view(shape), 'nstep': nstep, 'tnstep': nstep, 'lowest_step': lowest_step,
+    return {'result': lowest_x.view(shape), 'nstep': nstep, 'tnstep': tnstep, 'lowest_step': lowest_step,
             'diff': torch.norm(lowest_g).item(), 'diff_detail': torch.norm(lowest_g, dim=1),
             'prot_break': prot_break, 'trace': trace, 'eps': eps_s, 'threshold': threshold}
 

@@ -391,6 +391,21 @@ def prot_break_deep_batch(seed=6):
     return x
 
 
+def line_search_problem(kind, k=1.0):
+    """(arch, state_dict) of the line-search fixtures (tests/golden/make_golden_edges.py line_search_case): the root
+    problem of block 0.  'cifar_small': CIFAR10_SMALL as is.  'power' / 'toy': block 0's nets (nnet_x, nnet_z) with every
+    InducedNormLinear weight x k under a Lipschitz cap of 1000 (W_eff == W), a harder root problem on which the Armijo
+    search accepts backtracked steps."""
+    if kind == 'cifar_small':
+        return CIFAR10_SMALL, make_state_dict(CIFAR10_SMALL, 0)
+    arch = POWER if kind == 'power' else TOY
+    sd = make_state_dict(arch, 0)
+    for key in list(sd):
+        if key.startswith(('chain.0.nnet_x.', 'chain.0.nnet_z.')) and key.endswith('.weight'):
+            sd[key] = sd[key] * float(k)
+    return dict(arch, coeff=1000.), sd
+
+
 def perturbed_weight(sd, key, seed=1, scale=0.05):
     """sd[key + '.weight'] moved off its converged u / v (as after an optimiser step): W + scale * std(W) * N(0, 1),
     deterministic (numpy PCG64 keyed like the weights).  Power-iteration fixtures start from it."""

@@ -77,6 +77,8 @@ typedef struct InfBroydenStats {  /* mirrors the dict returned by broyden() (bro
   int* sample_nstep;
   int* sample_lowest_step;
   int* sample_prot_break;
+  /* nstep + the extra iterations of accepted line searches (broyden.py:156; == nstep without INF_OPT_LINE_SEARCH) */
+  int tnstep;
 } InfBroydenStats;
 
 /* ---- library ------------------------------------------------------------------------------ */
@@ -152,6 +154,12 @@ int inf_net_get_mfma(const InfNet* net);
  *                         layers or d = 2 with 1) as one launch for both nets: one forward pass keeping act' in registers,
  *                         then every term's VJP through the transposed weights' planes, dotted with the probe in the same
  *                         launch; 0 runs one GEMM launch per layer and term.
+ *   INF_OPT_LINE_SEARCH   read on the net whose root is solved: 0 (default, the reference's call sites: broyden(...)
+ *                         without ls) / 1: broyden(..., ls=True) -- each step's size from line_search(on=True) and
+ *                         scalar_search_armijo (broyden.py:24-99; quadratic then cubic backtracking, c1 1e-4, amin 1e-2),
+ *                         every trial point's norm read back; stats.tnstep counts the accepted searches' iterations
+ *                         (:156).  The global rule only (INF_ERR_UNSUPPORTED with INF_CONV_PER_SAMPLE); the fc block
+ *                         kernel is not used with it.
  * Unknown values of INFLOW_FUSED_K128 (0-3), INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP / INFLOW_FC_SERIES (0/1) and INFLOW_CONVERGENCE (global/per_sample)
  * make inf_net_create fail with INF_ERR_INVALID.
  * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
@@ -159,7 +167,7 @@ int inf_net_get_mfma(const InfNet* net);
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
   INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4,
-  INF_OPT_FC_BLOCK = 5, INF_OPT_FC_SERIES = 6
+  INF_OPT_FC_BLOCK = 5, INF_OPT_FC_SERIES = 6, INF_OPT_LINE_SEARCH = 7
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);
@@ -193,6 +201,10 @@ size_t inf_broyden_workspace_bytes(int batch, int d, int threshold);
 int inf_broyden_update(float* U, float* VT, const float* dx, const float* dg, const float* gx, const float* x,
                        float* update, float* x_next, float* dx_next, int batch, int d, int threshold, int nstep,
                        void* ws, size_t ws_bytes, void* stream);
+/* The trial point of a caller-driven line search (broyden(..., ls=True), broyden.py:79,94,99): x_est = x0 + step * update
+ * and dx = x_est - x0 over n floats, the product and the sum rounded separately as the reference's tensor ops do. */
+int inf_broyden_line_step(const float* x0, const float* update, float step, float* x_est, float* dx, size_t n,
+                          void* stream);
 /* imBlock forward value: z* = RootFind(nnet_z, nnet_x, x); z = (nnet_x(x) - nnet_z(z*)) + x
  * (implicit_block.py:226-227). */
 int inf_imblock_forward(InfNet* net_x, InfNet* net_z, const float* x, float* z, int batch, int threshold,

@@ -113,9 +113,57 @@ def _matvec(Us, VTs, x):
     return -x + torch.einsum('bij, bj -> bi', Us, VTx)
 
 
-def broyden(g_, x0, threshold, eps):
-    """Good-Broyden inverse-Jacobian root solve, line search off (broyden.py:123-193,
-    line_search(on=False) = broyden.py:66-99 with s = 1)."""
+def armijo_backtrack(phi, phi0):
+    """scalar_search_armijo (broyden.py:24-63) as line_search(on=True) calls it (:89): derphi0 = -phi0, c1 = 1e-4,
+    alpha0 = 1, amin = 1e-2.  phi: step -> ||g(x0 + step update)||^2 as a 0-d fp32 tensor (or inf); the arithmetic is
+    the reference's 0-d fp32 tensor arithmetic.  Returns (accepted step or None, cubic iterations)."""
+    der = -phi0
+    pa0 = phi(1)
+    if pa0 <= phi0 + 1e-4 * der:                                   # Armijo at the full step
+        return 1, 0
+    a0 = 1
+    a1 = -der * a0 ** 2 / 2.0 / (pa0 - phi0 - der * a0)            # minimiser of the quadratic interpolant
+    pa1 = phi(a1)
+    n = 0
+    while a1 > 1e-2:
+        r0, r1 = pa0 - phi0 - der * a0, pa1 - phi0 - der * a1
+        den = a0 ** 2 * a1 ** 2 * (a1 - a0)
+        ca = (a0 ** 2 * r1 - a1 ** 2 * r0) / den                   # cubic interpolant through phi0, pa0, pa1
+        cb = (-a0 ** 3 * r1 + a1 ** 3 * r0) / den
+        a2 = (-cb + torch.sqrt(torch.abs(cb ** 2 - 3 * ca * der))) / (3.0 * ca)
+        pa2 = phi(a2)
+        n += 1
+        if pa2 <= phi0 + 1e-4 * a2 * der:
+            return a2, n
+        if (a1 - a2) > a1 / 2.0 or (1 - a2 / a1) < 0.96:           # safeguard: halve
+            a2 = a1 / 2.0
+        a0, a1, pa0, pa1 = a1, a2, pa1, pa2
+    return None, n
+
+
+def line_search_step(g, x0, g0, update):
+    """line_search(update, x0, g0, g, on=True) (broyden.py:66-99): the step of the Armijo search (a failed search takes
+    the full step and reports no iterations), the last evaluation reused when the step is the stored one.
+    Returns x_est, g(x_est), x_est - x0, g(x_est) - g0, iterations."""
+    store = {'s': 0, 'phi': torch.norm(g0) ** 2, 'g': g0}
+
+    def phi(s):
+        if s == store['s']:
+            return store['phi']
+        gn = g(x0 + s * update)
+        store.update(s=s, g=gn, phi=torch.norm(gn) ** 2 if torch.isfinite(gn).all() else np.inf)
+        return store['phi']
+    s, n = armijo_backtrack(phi, store['phi'])
+    if s is None:
+        s, n = 1.0, 0
+    x_est = x0 + s * update
+    gn = store['g'] if s == store['s'] else g(x_est)
+    return x_est, gn, x_est - x0, gn - g0, n
+
+
+def broyden(g_, x0, threshold, eps, ls=False):
+    """Good-Broyden inverse-Jacobian root solve (broyden.py:123-193); ls=False: line_search(on=False) = broyden.py:66-99
+    with s = 1; ls=True: line_search_step (the Armijo search), tnstep counting its iterations (:156)."""
     shape = x0.shape
     x0 = x0.view(shape[0], -1)
     bsz, d = x0.size()
@@ -126,7 +174,7 @@ def broyden(g_, x0, threshold, eps):
 
     x_est = x0
     gx = g(x_est)
-    nstep = 0
+    nstep = tnstep = 0
     Us = torch.zeros(bsz, d, threshold)
     VTs = torch.zeros(bsz, threshold, d)
     update = -gx                                                  # :144
@@ -136,11 +184,15 @@ def broyden(g_, x0, threshold, eps):
     lowest = new_objective
     lowest_xest, lowest_gx, lowest_step = x_est, gx, nstep
     while new_objective >= eps and nstep < threshold:             # :153
-        x_new = x_est + update                                    # line_search(on=False), :94-99
-        gx_new = g(x_new)
-        delta_x, delta_gx = x_new - x_est, gx_new - gx
+        if ls:
+            x_new, gx_new, delta_x, delta_gx, n = line_search_step(g, x_est, gx, update)
+        else:
+            x_new = x_est + update                                # line_search(on=False), :94-99
+            gx_new = g(x_new)
+            delta_x, delta_gx, n = x_new - x_est, gx_new - gx, 0
         x_est, gx = x_new, gx_new
         nstep += 1
+        tnstep += n + 1
         new_objective = torch.norm(gx).item()
         trace.append(new_objective)
         if new_objective < lowest:                                # :159-162
@@ -164,7 +216,7 @@ def broyden(g_, x0, threshold, eps):
         VTs[:, m] = vT
         Us[:, :, m] = u
         update = -_matvec(Us[:, :, :nstep], VTs[:, :nstep], gx)   # :181
-    return {"result": lowest_xest.view(shape), "nstep": nstep, "lowest_step": lowest_step,
+    return {"result": lowest_xest.view(shape), "nstep": nstep, "tnstep": tnstep, "lowest_step": lowest_step,
             "diff": torch.norm(lowest_gx).item(), "diff_detail": torch.norm(lowest_gx, dim=1),
             "prot_break": prot_break, "trace": trace, "eps": eps, "threshold": threshold}
 

@@ -21,6 +21,12 @@ container only; same harness as make_golden.py: its import shims, model builders
   prot_break_deep_b6   the same on the POWER nets' shape (PROT_BREAK_DEEP: the fused fc and block-kernel paths)
   cifar_small_b4_ps    per-sample convergence: the reference's broyden run on each sample as a batch of one
   cifar_full_b8_ps     (the root solves; probes and series lengths as in the batched run)
+  line_search_*        broyden(g, 0, 30, eps, ls=True) (broyden.py:24-99,123-193) on an imBlock's root problem
+                       g(z) = x_embed - f_z(z) - z (implicit_block.py:67-73): a CIFAR idim-64 block (every search after
+                       the first accepts the full step; the first fails after 4 cubic iterations and takes it anyway),
+                       a POWER block and a toy block with their nets' weights x k under a Lipschitz cap of 1000, where
+                       backtracking steps are accepted: nstep, tnstep, lowest_step, trace, the accepted step sizes and
+                       the result
 """
 import logging
 import os
@@ -436,6 +442,51 @@ def prot_break_case(seed=5, deep=False):
     _save('prot_break_deep_b6' if deep else 'prot_break_b6', out)
 
 
+# ---- N4: Broyden with the line search ---------------------------------------------------------------------
+def line_search_case(name, kind, B, seed, k=None, threshold=30):
+    import lib.layers.broyden as rb               # the reference's
+    steps = []
+    orig = rb.scalar_search_armijo
+
+    def armijo(phi, phi0, derphi0, c1=1e-4, alpha0=1, amin=0):
+        r = orig(phi, phi0, derphi0, c1, alpha0, amin)
+        steps.append((-1.0 if r[0] is None else float(r[0]), int(r[2])))
+        return r
+    rb.scalar_search_armijo = armijo
+    try:
+        if kind == 'cifar_small':
+            blk = _block(syn.CIFAR10_SMALL, B, 0)
+            x = 0.5 * torch.randn(B, 3, 32, 32, generator=torch.Generator().manual_seed(seed))
+        else:
+            arch = syn.POWER if kind == 'power' else syn.TOY
+            model = mg.fc_model(arch)
+            model.load_state_dict(syn.make_state_dict(arch, 0), strict=True)
+            model.eval()
+            blk = [m for m in model.modules() if isinstance(m, ib.imBlock)][0]
+            with torch.no_grad():
+                for net in (blk.nnet_x, blk.nnet_z):
+                    for m in net.modules():
+                        if hasattr(m, 'coeff'):
+                            m.coeff = 1000.
+                            m.weight.mul_(k)
+            x = syn.tabular_batch(B, arch['d'], seed=seed)
+        eps = float(blk.eps_forward)
+        with torch.no_grad():
+            x_embed = blk.nnet_x(x) + x
+            r = rb.broyden(lambda z: x_embed - blk.nnet_z(z) - z, torch.zeros_like(x), threshold, eps, ls=True)
+    finally:
+        rb.scalar_search_armijo = orig
+    out = dict(x=x.numpy(), seed=np.int64(seed), kind=np.array(kind), k=np.float64(k or 1.0),
+               threshold=np.int64(threshold), eps=np.float64(eps), nstep=np.int64(r['nstep']),
+               tnstep=np.int64(r['tnstep']), lowest_step=np.int64(r['lowest_step']),
+               prot_break=np.int64(r['prot_break']), trace=np.array([float(t) for t in r['trace']]),
+               steps=np.array([a for a, _ in steps]), step_iters=np.array([i for _, i in steps], dtype=np.int64),
+               result=r['result'].numpy().astype(np.float32), diff=np.float64(r['diff']))
+    print('%-24s nstep %d tnstep %d lowest %d steps %s' % (name, r['nstep'], r['tnstep'], r['lowest_step'],
+                                                          [(round(a, 4), i) for a, i in steps]))
+    _save(name, out)
+
+
 CASES = {
     'prot_break_b6': prot_break_case,
     'prot_break_deep_b6': lambda: prot_break_case(seed=6, deep=True),
@@ -453,6 +504,9 @@ CASES = {
                                                  wrap_broyden=per_sample_broyden),
     'cifar_full_b8_ps': lambda: _eval_flow_case('cifar_full_b8_ps', syn.CIFAR10, 8, 11,
                                                 wrap_broyden=per_sample_broyden),
+    'line_search_cifar_small_b4': lambda: line_search_case('line_search_cifar_small_b4', 'cifar_small', 4, 3),
+    'line_search_power_b16': lambda: line_search_case('line_search_power_b16', 'power', 16, 4, k=2.0),
+    'line_search_toy_b16': lambda: line_search_case('line_search_toy_b16', 'toy', 16, 3, k=2.2),
 }
 
 if __name__ == '__main__':

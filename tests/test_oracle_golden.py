@@ -81,3 +81,41 @@ def test_oracle_protective_break_matches_reference(golden_dir):
         assert breaks == [int(v) for v in g['ps_prot_break']]
         z = fx(x) - fz(torch.cat(rows)) + x
         np.testing.assert_allclose(z.numpy(), g['ps_z'], rtol=0, atol=2e-5 * max(1., float(np.abs(g['ps_z']).max())))
+
+
+LINE_SEARCH = ['line_search_cifar_small_b4', 'line_search_power_b16', 'line_search_toy_b16']
+
+
+@pytest.mark.parametrize('name', LINE_SEARCH)
+def test_oracle_line_search_matches_reference(golden_dir, name):
+    """The oracle's broyden(..., ls=True) (line_search_step / armijo_backtrack, broyden.py:24-99) on block 0's root
+    problem g(z) = x_embed - f_z(z) - z against the reference's run: nstep, tnstep, lowest_step, every search's accepted
+    step (None -> -1) and iterations exact, the root within 2e-5 of its max."""
+    path = os.path.join(golden_dir, name + '.npz')
+    if not os.path.exists(path):
+        pytest.skip('fixture %s not generated' % name)
+    g = np.load(path)
+    arch, sd = syn.line_search_problem(str(g['kind']), float(g['k']))
+    layout = syn.conv_flow_layout(arch) if arch['kind'] == 'conv' else syn.fc_flow_layout(arch)
+    blk = orc.build(arch, sd, layout).blocks()[0]
+    x = torch.from_numpy(g['x'])
+    steps = []
+    real = orc.armijo_backtrack
+
+    def spy(phi, phi0):
+        r = real(phi, phi0)
+        steps.append((-1.0 if r[0] is None else float(r[0]), r[1]))
+        return r
+    orc.armijo_backtrack = spy
+    try:
+        with torch.no_grad():
+            x_embed = blk.fx(x) + x
+            r = orc.broyden(lambda z: x_embed - blk.fz(z) - z, torch.zeros_like(x), int(g['threshold']),
+                            float(g['eps']), ls=True)
+    finally:
+        orc.armijo_backtrack = real
+    assert (r['nstep'], r['tnstep'], r['lowest_step']) == (int(g['nstep']), int(g['tnstep']), int(g['lowest_step']))
+    assert [i for _, i in steps] == [int(v) for v in g['step_iters']]
+    np.testing.assert_allclose([a for a, _ in steps], g['steps'], rtol=1e-4, atol=0)
+    res = r['result'].numpy()
+    np.testing.assert_allclose(res, g['result'], rtol=0, atol=2e-5 * max(1.0, float(np.abs(g['result']).max())))
