@@ -1640,6 +1640,43 @@ const char* inf_status_string(int s) {
 
 int inf_last_hip_error(void) { return inf::g_last_hip; }
 
+// Re-points a net at other tensors of the same layout (a DataParallel replica's copies of the parameters on another
+// device, lib/_hip native_net): the pointers the refresh and the launches read change, nothing is repacked -- the caller
+// refreshes only when the values differ from the last refresh's.
+int inf_net_set_tensors(InfNet* n, const InfNetDesc* desc) {
+  if (!n || !desc || desc->n_layers <= 0 || !desc->layers) return INF_ERR_INVALID;
+  int i = 0;
+  const bool pre = desc->layers[0].kind == INF_ACT_SWISH || desc->layers[0].kind == INF_ACT_SIN;
+  if (pre != (n->pre_act != ACT_NONE)) return INF_ERR_INVALID;
+  if (pre) i = 1;
+  size_t l = 0;
+  std::vector<WLayer> L = n->L;
+  const float* pre_beta = pre ? desc->layers[0].beta : n->pre_beta;
+  for (; i < desc->n_layers; ++i) {
+    const InfLayerDesc& d = desc->layers[i];
+    if (d.kind == INF_LAYER_CONV || d.kind == INF_LAYER_LINEAR) {
+      if (l >= L.size()) return INF_ERR_INVALID;
+      WLayer& w = L[l++];
+      const int ks = d.kind == INF_LAYER_LINEAR ? 1 : d.ksize;
+      if (w.kind != d.kind || w.cin != d.cin || w.cout != d.cout || w.ks != ks || !d.weight || !d.bias || !d.u || !d.v)
+        return INF_ERR_INVALID;
+      w.W = d.weight;
+      w.b = d.bias;
+      w.u = d.u;
+      w.v = d.v;
+    } else if (d.kind == INF_ACT_SWISH || d.kind == INF_ACT_SIN) {
+      if (l == 0 || L[l - 1].act != (d.kind == INF_ACT_SWISH ? ACT_SWISH : ACT_SIN)) return INF_ERR_INVALID;
+      L[l - 1].act_beta = d.beta;
+    } else {
+      return INF_ERR_INVALID;
+    }
+  }
+  if (l != L.size()) return INF_ERR_INVALID;
+  n->L = L;
+  n->pre_beta = pre_beta;
+  return INF_OK;
+}
+
 int inf_net_create(const InfNetDesc* desc, InfNet** out) {
   if (!desc || !out || desc->n_layers <= 0 || !desc->layers) return INF_ERR_INVALID;
   InfNet* n = new (std::nothrow) InfNet();

@@ -328,7 +328,7 @@ __global__ void line_step_kernel(const float* x, const float* upd, float sc, flo
   dx[i] = __fsub_rn(xe, x0);
 }
 int launch_line_step(const float* x, const float* upd, float sc, float* xnew, float* dx, long n, hipStream_t s) {
-  INF_PROF_LAUNCH(s, 705, 16.0 * n, line_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, sc, xnew, dx, n);
+  INF_PROF_LAUNCH(s, 707, 16.0 * n, line_step_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, upd, sc, xnew, dx, n);
   return INF_OK;
 }
 __global__ void neg_kernel(const float* x, float* y, long n) {

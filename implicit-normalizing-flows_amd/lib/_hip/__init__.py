@@ -10,6 +10,7 @@ import atexit
 import ctypes
 import os
 import threading
+import weakref
 
 import torch
 
@@ -93,6 +94,7 @@ _SIGS = {
     'inf_net_create': (ctypes.c_int, [ctypes.POINTER(NetDesc), ctypes.POINTER(_P)]),
     'inf_net_destroy': (ctypes.c_int, [_P]),
     'inf_net_refresh': (ctypes.c_int, [_P, _P]),
+    'inf_net_set_tensors': (ctypes.c_int, [_P, ctypes.POINTER(NetDesc)]),
     'inf_net_set_mfma': (ctypes.c_int, [_P, ctypes.c_int]),
     'inf_net_get_mfma': (ctypes.c_int, [_P]),
     'inf_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int]),
@@ -231,27 +233,40 @@ def workspace(device, nbytes):
 class NativeNet:
     """An InfNet built from a flat list of (kind, module) entries of an nn.Sequential."""
 
+    created = 0                                    # inf_net_create / inf_net_refresh calls in this process (tests)
+    refreshed = 0
+
     def __init__(self, entries, shape, device):
         self.lib = load()
         self.device = device
         self.shape = tuple(shape)                  # (C, H, W) or (d,)
-        self._tensors = []
-        descs = []
+        nd, self._tensors, keep = self._desc(entries)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(self.lib.inf_net_create(ctypes.byref(nd), ctypes.byref(h)), 'inf_net_create')
+        NativeNet.created += 1
+        self.handle = h
+        self._stamp = None
+        self._lock = threading.Lock()
+        self.value_source = None                   # stamp() of the tensors the values come from (replicas: the owner's)
+        self.holder = None                         # weakref to the module whose tensors the net points at
+        self.ptrs = self.current_ptrs()
+
+    def _desc(self, entries):
+        tensors, descs = [], []
         for kind, m in entries:
             d = LayerDesc()
+            d.kind = kind
             if kind in (INF_LAYER_CONV, INF_LAYER_LINEAR):
                 w = m.weight
-                d.kind = kind
                 d.cin, d.cout = int(w.shape[1]), int(w.shape[0])
                 d.ksize = int(w.shape[2]) if kind == INF_LAYER_CONV else 1
                 d.weight, d.bias, d.u, d.v = ptr(w), ptr(m.bias), ptr(m.u), ptr(m.v)
                 d.coeff = float(m.coeff)
-                self._tensors += [w, m.bias, m.u, m.v]
-            else:
-                d.kind = kind
-                if kind == INF_ACT_SWISH:
-                    d.beta = ptr(m.beta)
-                    self._tensors.append(m.beta)
+                tensors += [w, m.bias, m.u, m.v]
+            elif kind == INF_ACT_SWISH:
+                d.beta = ptr(m.beta)
+                tensors.append(m.beta)
             descs.append(d)
         arr = (LayerDesc * len(descs))(*descs)
         nd = NetDesc()
@@ -261,24 +276,41 @@ class NativeNet:
             nd.channels, nd.height, nd.width = self.shape
         else:
             nd.channels, nd.height, nd.width = self.shape[0], 1, 1
-        h = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            check(self.lib.inf_net_create(ctypes.byref(nd), ctypes.byref(h)), 'inf_net_create')
-        self.handle = h
-        self._stamp = None
+        return nd, tensors, arr
+
+    def retarget(self, entries):
+        """Point the engine net at another module's tensors of the same layout (a DataParallel replica's parameter
+        copies): inf_net_set_tensors, no re-creation; refresh_if_needed repacks only if the values changed."""
+        nd, tensors, keep = self._desc(entries)
+        check(self.lib.inf_net_set_tensors(self.handle, ctypes.byref(nd)), 'inf_net_set_tensors')
+        self._tensors = tensors
         self.ptrs = self.current_ptrs()
 
     def current_ptrs(self):
         return tuple(t.data_ptr() for t in self._tensors)
 
+    @staticmethod
+    def _tensors_of(entries):
+        out = []
+        for kind, m in entries:
+            if kind in (INF_LAYER_CONV, INF_LAYER_LINEAR):
+                out += [m.weight, m.bias, m.u, m.v]
+            elif kind == INF_ACT_SWISH:
+                out.append(m.beta)
+        return out
+
     def stamp(self):
         return tuple((t.data_ptr(), t._version) for t in self._tensors)
 
     def refresh_if_needed(self, stream):
-        st = self.stamp()
-        if st != self._stamp:
-            check(self.lib.inf_net_refresh(self.handle, stream), 'inf_net_refresh')
-            self._stamp = st
+        """inf_net_refresh when the parameter values changed since the last refresh: judged by the (data_ptr, version)
+        stamp of the tensors the values come from -- the net's own, or for a replica's copies the owner module's."""
+        with self._lock:
+            st = self.value_source() if self.value_source is not None else self.stamp()
+            if st != self._stamp:
+                check(self.lib.inf_net_refresh(self.handle, stream), 'inf_net_refresh')
+                NativeNet.refreshed += 1
+                self._stamp = st
 
     def set_option(self, option, value):
         """inf_net_set_option; returns the previous value."""
@@ -333,8 +365,19 @@ def net_entries(seq):
 
 
 class _NativeCache(dict):
-    """Per-module cache of engine nets.  Not copied or pickled with the module: a deep copy (or an
-    unpickled module) builds its own engine nets from its own parameter tensors on first use."""
+    """Per-module cache of engine nets, keyed (device index, per-sample shape).  Not copied or pickled with the module: a
+    deep copy (or an unpickled module) builds its own engine nets from its own parameter tensors on first use.
+
+    DataParallel (train_img.py:203-204,820): replicate() gives each replica a shallow copy of the module's __dict__, so
+    the replicas share this cache with the module that owns it (attach_cache puts it there at construction, before any
+    replication).  A replica's parameters are copies (other devices) or the owner's tensors themselves (the owner's
+    device): its net is looked up by device, re-pointed at the replica's tensors when they differ (no re-creation), and
+    repacked only when the owner's parameters changed.  The replicas run in threads: lookups and refreshes hold locks."""
+
+    def __init__(self, owner=None):
+        super().__init__()
+        self.lock = threading.RLock()
+        self.owner = weakref.ref(owner) if owner is not None else None
 
     def __deepcopy__(self, memo):
         return _NativeCache()
@@ -343,26 +386,59 @@ class _NativeCache(dict):
         return (_NativeCache, ())
 
 
+def attach_cache(module):
+    """Give `module` its engine-net cache now (its constructor calls this), so that DataParallel replicas share it."""
+    if not isinstance(module.__dict__.get('_inf_native'), _NativeCache):
+        module.__dict__['_inf_native'] = _NativeCache(module)
+    return module.__dict__['_inf_native']
+
+
+def _unsupported(module):
+    return HipError('net %s is not supported by the MI355X engine (supported: nn.Sequential of InducedNormConv2d '
+                    '(stride 1, k in {1,3}) / InducedNormLinear with Swish / Sin)' % type(module).__name__)
+
+
 def native_net(module, shape, device):
     """Cached NativeNet for `module` acting on per-sample `shape` on `device`."""
     cache = module.__dict__.get('_inf_native')
     if not isinstance(cache, _NativeCache):
-        cache = module.__dict__['_inf_native'] = _NativeCache()
-    key = (torch.device(device).index, tuple(shape))
-    net = cache.get(key) or cache.get((key[0], (int(torch.Size(shape).numel()),)))
-    if net is not None and net.current_ptrs() == net.ptrs:
+        cache = attach_cache(module)
+    with cache.lock:
+        owner = cache.owner() if cache.owner is not None else None
+        if owner is None:                              # a deep copy's fresh cache, or the owner is gone
+            cache.owner = weakref.ref(module)
+            owner = module
+        key = (torch.device(device).index, tuple(shape))
+        net = cache.get(key) or cache.get((key[0], (int(torch.Size(shape).numel()),)))
+        if net is not None and net.holder is not None and net.holder() is module and net.current_ptrs() == net.ptrs:
+            return net
+        entries = net_entries(module)
+        if entries is None:
+            raise _unsupported(module)
+        if net is None:
+            if entries and all(k != INF_LAYER_CONV for k, _ in entries):
+                shape = (int(torch.Size(shape).numel()),)     # fc nets act on the flattened sample
+                key = (key[0], tuple(shape))
+            net = NativeNet(entries, shape, device)
+            cache[key] = net
+        elif tuple(t.data_ptr() for t in NativeNet._tensors_of(entries)) != net.ptrs:
+            net.retarget(entries)                      # a replica's copies, or back to the owner's tensors
+        net.holder = weakref.ref(module)
+        net.value_source = None if module is owner else _owner_stamp(owner)
         return net
-    entries = net_entries(module)
-    if entries is not None and entries and all(k != INF_LAYER_CONV for k, _ in entries):
-        shape = (int(torch.Size(shape).numel()),)     # fc nets act on the flattened sample
-        key = (key[0], tuple(shape))
-    if entries is None:
-        raise HipError('net %s is not supported by the MI355X engine (supported: nn.Sequential of '
-                       'InducedNormConv2d (stride 1, k in {1,3}) / InducedNormLinear with Swish / Sin)'
-                       % type(module).__name__)
-    net = NativeNet(entries, shape, device)
-    cache[key] = net
-    return net
+
+
+def _owner_stamp(owner):
+    """The stamp of the owner module's parameter tensors (a replica's values are copies of them)."""
+    ref = weakref.ref(owner)
+
+    def stamp():
+        o = ref()
+        entries = net_entries(o) if o is not None else None
+        if entries is None:
+            return None
+        return tuple((t.data_ptr(), t._version) for t in NativeNet._tensors_of(entries))
+    return stamp
 
 
 def profile_begin(max_launches=200000):
@@ -382,7 +458,7 @@ def profile_end():
 # rocprofv3 Kernel_Name without namespace, template arguments and signature)
 PHASE_TAGS = {
     700: 'resid_bcast_kernel', 701: 'resid_bcast_fc_kernel', 702: 'broyden_start_fc_kernel', 703: 'axpy_step_kernel',
-    704: 'neg_kernel', 705: 'reduce_partials_kernel', 706: 'recomp_kernel',
+    704: 'neg_kernel', 705: 'reduce_partials_kernel', 706: 'recomp_kernel', 707: 'line_step_kernel',
     710: 'broyden_p1', 711: 'broyden_p2', 712: 'broyden_p3', 713: 'broyden_p4', 714: 'br_sum_chunks',
     715: 'broyden_small_d_kernel',
     720: 'series_combine_kernel', 721: 'rademacher_kernel',

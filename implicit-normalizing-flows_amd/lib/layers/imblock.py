@@ -379,6 +379,8 @@ class imBlock(nn.Module):
         super().__init__()
         self.nnet_x = nnet_x
         self.nnet_z = nnet_z
+        for net in (nnet_x, nnet_z):       # engine-net caches shared with DataParallel replicas (lib/_hip)
+            _hip.attach_cache(net)
         # frozen copies, kept for state-dict compatibility (implicit_block.py:136-141)
         self.nnet_x_copy = copy.deepcopy(nnet_x)
         self.nnet_z_copy = copy.deepcopy(nnet_z)

@@ -66,6 +66,7 @@ class iResBlock(nn.Module):
                  n_samples=1, n_exact_terms=2, n_dist='geometric', neumann_grad=True, grad_in_forward=False):
         super().__init__()
         self.nnet = nnet
+        _hip.attach_cache(nnet)            # engine-net cache shared with DataParallel replicas (lib/_hip)
         self.n_dist = n_dist
         self.geom_p = nn.Parameter(torch.tensor(np.log(geom_p) - np.log(1. - geom_p)))
         self.lamb = nn.Parameter(torch.tensor(lamb))

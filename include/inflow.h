@@ -98,6 +98,11 @@ int inf_net_destroy(InfNet* net);
  * sigma = u.(W v) on device, W_eff = W / max(1, sigma/coeff), repacked for the MFMA kernels.
  * Call after any parameter change (the Python side tracks tensor versions). */
 int inf_net_refresh(InfNet* net, void* stream);
+/* Re-points the net at other tensors of the same layout (same layer kinds, shapes and activations as at create), e.g. a
+ * DataParallel replica's copies of the parameters (train_img.py:203-204 nn.DataParallel): weight / bias / u / v / beta
+ * pointers only, nothing repacked -- call inf_net_refresh when the values differ from the last refresh's.
+ * INF_ERR_INVALID when the layout differs (the net is left unchanged). */
+int inf_net_set_tensors(InfNet* net, const InfNetDesc* desc);
 /* Arithmetic of the fused 3-1-3 conv kernel's three contractions (fused313.hip phases A, B, C).
  *   INF_MFMA_F32    v_mfma_f32_32x32x2_f32: exact fp32 products, k-ordered fp32 accumulation.
  *   INF_MFMA_BF16X6 both operands split exactly into three bf16 pieces (x = hi + mid + lo, truncation),
