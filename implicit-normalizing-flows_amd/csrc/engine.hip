@@ -1436,13 +1436,16 @@ int fc_block_eval(InfNet* nx, InfNet* nz, const float* x, float* z, float* logde
 
 // ---------------------------------------------------------------------------------------------
 // Parameter gradients (training path) on the generic GEMM operands (W_eff packed at refresh).
-// Conv nets whose intermediate activations are swish: layer l computes h_l = W_l * in_l + b_l,
-// in_0 = preact(x), in_l = swish(h_{l-1}) (applied on load from the stored pre-activation).
+// Nets whose intermediate activations are Swish or Sin: layer l computes h_l = W_l * in_l + b_l,
+// in_0 = preact(x), in_l = act(h_{l-1}) (applied once from the stored pre-activation).  Conv nets in their (B, C, H, W)
+// layout; fc nets feature-major (d, N), N columns as one image of N pixels (gemm_base) -- the C-ABI entries transpose
+// the (B, d) boundary tensors in and out.
 // ---------------------------------------------------------------------------------------------
 struct GradBufs {
   std::vector<float*> H, Hd, Ad;     // pre-activations, their tangents, activation tangents (Ad[0]: input)
-  std::vector<float*> A;             // layer inputs after their swish (A[0] = preact(x)), computed once per call
+  std::vector<float*> A;             // layer inputs after their activation (A[0] = preact(x)), computed once per call
   float *gA, *gB, *hA, *hB, *gad, *ga, *Y, *slab, *dWe, *dWe2, *dsig, *xin, *tmp_in, *act;
+  float *x_t, *w_t, *e_t, *gx_t;     // fc nets: the internal-layout (d, N) copies of the boundary inputs / x-gradient
   double *bpart, *dot;
   int max_split;
 };
@@ -1471,6 +1474,7 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
   g.dsig = w.take<float>(mn);
   g.xin = w.take<float>(in);
   g.tmp_in = w.take<float>(in);
+  for (float** p : {&g.x_t, &g.w_t, &g.e_t, &g.gx_t}) *p = n->fc ? w.take<float>(in) : nullptr;
   g.act = w.take<float>(std::max(hid, in));   // swish of a stored pre-activation (weight-gradient operand)
   g.bpart = w.take<double>(std::max<size_t>(GRAD_BLOCKS + 64, glue_batched_dot_scratch(B, (long)n->hidden_max * n->P) + 64));
   g.dot = w.take<double>(128);      // [0] the dot, [1..64] its block partials
@@ -1482,13 +1486,14 @@ size_t carve_grad(const InfNet* n, int B, void* ws, size_t cap, GradBufs& g) {
 // applied once into gb.A[l] instead of in every output tile's loader.  Returns the operand, no beta left.
 static int layer_input(InfNet* n, int l, const float* x, GradBufs& gb, int B, hipStream_t s, const float** out) {
   const float* in = l == 0 ? x : gb.H[l - 1];
+  const int act = l == 0 ? n->pre_act : n->L[l - 1].act;
   const float* pb = l == 0 ? n->pre_beta : n->L[l - 1].act_beta;
-  if (!pb) {
+  if (act == ACT_NONE) {
     *out = in;
     return INF_OK;
   }
   const long ne = (long)B * n->L[l].cin * n->P;
-  INF_TRY(launch_swish_apply(in, pb, gb.A[l], ne, s));
+  INF_TRY(launch_act_apply(in, act, pb, gb.A[l], ne, s));
   *out = gb.A[l];
   return INF_OK;
 }
@@ -1534,14 +1539,14 @@ static int layer_wgrad(InfNet* n, int l, const float* G, const float* X, const f
   WgradArgs a;
   memset(&a, 0, sizeof(a));
   a.G = G;
-  a.g_sample = (long)w.cout * n->P;
   a.X = X;
-  a.x_sample = (long)w.cin * n->P;
   a.x_beta = x_beta;
-  a.B = B;
-  a.P = n->P;
-  a.H = n->H;
-  a.W = n->W;
+  a.B = n->fc ? 1 : B;               // fc: one image of B columns
+  a.P = n->fc ? B : n->P;
+  a.H = n->fc ? 1 : n->H;
+  a.W = n->fc ? B : n->W;
+  a.g_sample = (long)w.cout * a.P;
+  a.x_sample = (long)w.cin * a.P;
   a.ks = w.ks;
   a.M = w.cout;
   a.N = w.cin * w.ks * w.ks;
@@ -1576,10 +1581,11 @@ static int layer_sigma_chain(InfNet* n, int l, const float* dWe, float* dW, Grad
 }
 
 static bool grad_supported(const InfNet* n) {
-  if (n->fc || n->L.empty()) return false;
+  if (n->L.empty()) return false;
   for (size_t l = 0; l + 1 < n->L.size(); ++l)
-    if (n->L[l].act != ACT_SWISH) return false;
+    if (n->L[l].act != ACT_SWISH && n->L[l].act != ACT_SIN) return false;
   if (n->L.back().act != ACT_NONE) return false;
+  if (n->fc && n->pre_act != ACT_NONE) return false;
   return n->pre_act == ACT_NONE || n->pre_act == ACT_SWISH;
 }
 
@@ -1595,7 +1601,7 @@ static int layer_param_grads(InfNet* n, int l, const float* G_tan, const float* 
     const long mn = (long)w.cout * w.cin * w.ks * w.ks;
     // the primal operand's swish once per element, not inside every output tile's loader
     if (G_pri && X_pri_beta) {
-      INF_TRY(launch_swish_apply(X_pri, X_pri_beta, gb.act, (long)B * w.cin * n->P, s));
+      INF_TRY(launch_act_apply(X_pri, ACT_SWISH, X_pri_beta, gb.act, (long)B * w.cin * n->P, s));
       X_pri = gb.act;
       X_pri_beta = nullptr;
     }
@@ -1612,7 +1618,7 @@ static int layer_param_grads(InfNet* n, int l, const float* G_tan, const float* 
   }
   float* db = grad_out(gr->db, l);
   if (db) {
-    if (G_pri) INF_TRY(launch_channel_sum(G_pri, B, w.cout, n->P, db, s));
+    if (G_pri) INF_TRY(n->fc ? launch_channel_sum(G_pri, 1, w.cout, B, db, s) : launch_channel_sum(G_pri, B, w.cout, n->P, db, s));
     else INF_HIP(hipMemsetAsync(db, 0, sizeof(float) * w.cout, s));
   }
   return INF_OK;
@@ -2988,15 +2994,13 @@ int inf_rademacher(float* out, size_t n, uint64_t seed, uint64_t offset, void* s
   if (!out && n) return INF_ERR_INVALID;
   return glue_rademacher(out, n, seed, offset, (hipStream_t)stream);
 }
-// Gradient of sum(gout * f(x)) with respect to every parameter of a conv net (and x): the recompute
-// graph of the training forward (implicit_block.py:226-227) and the first-order terms of any caller.
-int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, const InfNetGrads* gr, int B,
-                       void* ws, size_t ws_bytes, void* stream) {
-  if (!n || !x || !gout || !gr || B <= 0) return INF_ERR_INVALID;
-  if (!grad_supported(n)) return INF_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
-  GradBufs gb;
-  if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
+}  // extern "C"
+
+namespace {
+// sum(gout * f(x)) differentiated into every parameter (and x, into gx when given) on internal-layout tensors: conv
+// (B, C, H, W), fc (d, B)
+int param_grad_core(InfNet* n, const float* x, const float* gout, float* gx, const InfNetGrads* gr, int B, GradBufs& gb,
+                    hipStream_t s) {
   const int L = (int)n->L.size();
   const long hidP = (long)n->P;
   // forward: pre-activations (each layer's input activated once, gb.A)
@@ -3015,16 +3019,16 @@ int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, 
       const long ne = (long)B * prev.cout * hidP;
       INF_TRY(layer_vjp(n, l, g, gb.ga, B, gb, s));
       float* gp = bufs[l & 1];
-      INF_TRY(launch_act_bwd1(gb.ga, gb.H[l - 1], prev.act_beta, gp, gb.bpart, ne, GRAD_BLOCKS, s));
+      INF_TRY(launch_act_bwd1(gb.ga, gb.H[l - 1], prev.act, prev.act_beta, gp, gb.bpart, ne, GRAD_BLOCKS, s));
       float* dbeta = grad_out(gr->dbeta, l - 1);
-      if (dbeta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
+      if (dbeta && prev.act == ACT_SWISH) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
       g = gp;
     } else if (gx || (n->pre_beta && gr->dpre_beta)) {
       const long ne = (long)B * n->d;
       float* gin = gx ? gx : gb.tmp_in;
       if (n->pre_beta) {
         INF_TRY(layer_vjp(n, 0, g, gb.ga, B, gb, s));
-        INF_TRY(launch_act_bwd1(gb.ga, x, n->pre_beta, gin, gb.bpart, ne, GRAD_BLOCKS, s));
+        INF_TRY(launch_act_bwd1(gb.ga, x, ACT_SWISH, n->pre_beta, gin, gb.bpart, ne, GRAD_BLOCKS, s));
         if (gr->dpre_beta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, gr->dpre_beta, 0, s));
       } else {
         INF_TRY(layer_vjp(n, 0, g, gin, B, gb, s));
@@ -3033,24 +3037,41 @@ int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, 
   }
   return INF_OK;
 }
+}  // namespace
 
-// Gradient of s = sum_b w_b^T J(x_b) eps_b (w fixed) with respect to x and every parameter, and the value
-// s_b per sample: the memory-efficient Neumann estimator's surrogate (implicit_block.py:388-394,437-438),
-// forward-over-reverse on the engine.
-int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const float* eps, float* value, float* gx,
-                           const InfNetGrads* gr, int B, void* ws, size_t ws_bytes, void* stream) {
-  if (!n || !x || !w || !eps || !gr || B <= 0) return INF_ERR_INVALID;
+extern "C" {
+// Gradient of sum(gout * f(x)) with respect to every parameter of the net (and x): the recompute graph of the training
+// forward (implicit_block.py:226-227) and the first-order terms of any caller.  Conv nets (Swish) and fc nets (Swish /
+// Sin; x, gout, gx in the (B, d) boundary layout).
+int inf_net_param_grad(InfNet* n, const float* x, const float* gout, float* gx, const InfNetGrads* gr, int B,
+                       void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !gout || !gr || B <= 0) return INF_ERR_INVALID;
   if (!grad_supported(n)) return INF_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   GradBufs gb;
   if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
+  if (!n->fc) return param_grad_core(n, x, gout, gx, gr, B, gb, s);
+  INF_TRY(launch_transpose(x, gb.x_t, B, n->d, s));
+  INF_TRY(launch_transpose(gout, gb.w_t, B, n->d, s));
+  INF_TRY(param_grad_core(n, gb.x_t, gb.w_t, gx ? gb.gx_t : nullptr, gr, B, gb, s));
+  if (gx) INF_TRY(launch_transpose(gb.gx_t, gx, n->d, B, s));
+  return INF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// s = sum_b w_b^T J(x_b) eps_b (w, eps fixed) differentiated into x (gx) and every parameter, forward-over-reverse, on
+// internal-layout tensors; the per-sample value s_b (conv nets only: value non-null)
+int surrogate_core(InfNet* n, const float* x, const float* w, const float* eps, float* value, float* gx,
+                   const InfNetGrads* gr, int B, GradBufs& gb, hipStream_t s) {
   const int L = (int)n->L.size();
   const long nin = (long)B * n->d;
   // input tangent: eps * preact'(x) (or eps)
   const float* in_tan = eps;
   if (n->pre_beta) {
     INF_HIP(hipMemcpyAsync(gb.Ad[0], eps, sizeof(float) * nin, hipMemcpyDeviceToDevice, s));
-    INF_TRY(launch_act_tangent(gb.Ad[0], x, n->pre_beta, nin, s));
+    INF_TRY(launch_act_tangent(gb.Ad[0], x, ACT_SWISH, n->pre_beta, nin, s));
     in_tan = gb.Ad[0];
   }
   // forward: primal pre-activations H, tangents Hd, activation tangents Ad
@@ -3062,7 +3083,7 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
     INF_TRY(layer_fwd(n, l, tin, nullptr, false, gb.Hd[l], B, s));
     const long ne = (long)B * n->L[l].cout * n->P;
     INF_HIP(hipMemcpyAsync(gb.Ad[l + 1], gb.Hd[l], sizeof(float) * ne, hipMemcpyDeviceToDevice, s));
-    INF_TRY(launch_act_tangent(gb.Ad[l + 1], gb.H[l], n->L[l].act_beta, ne, s));
+    INF_TRY(launch_act_tangent(gb.Ad[l + 1], gb.H[l], n->L[l].act, n->L[l].act_beta, ne, s));
   }
   // reverse: G_tan = gbar of the layer's tangent output, G_pri = gbar of its primal output
   const float* G_tan = w;
@@ -3087,18 +3108,18 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
       const long ne = (long)B * prev.cout * n->P;
       float* nt = tb[l & 1];
       float* np = pb2[l & 1];
-      INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, gb.H[l - 1], gb.Hd[l - 1], prev.act_beta, nt, np,
-                              gb.bpart, ne, GRAD_BLOCKS, s));
+      INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, gb.H[l - 1], gb.Hd[l - 1], prev.act, prev.act_beta, nt,
+                              np, gb.bpart, ne, GRAD_BLOCKS, s));
       float* dbeta = grad_out(gr->dbeta, l - 1);
-      if (dbeta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
+      if (dbeta && prev.act == ACT_SWISH) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, dbeta, 0, s));
       G_tan = nt;
       G_pri = np;
     } else {
       float* gin = gx ? gx : gb.tmp_in;
       if (n->pre_beta) {
         // x-gradient: gbar_adot eps s''(x) + gbar_a s'(x); beta: ... (act_bwd2 with h = x, hdot = eps)
-        INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, x, eps, n->pre_beta, gb.xin, gin, gb.bpart, nin,
-                                GRAD_BLOCKS, s));
+        INF_TRY(launch_act_bwd2(gb.gad, G_pri ? gb.ga : nullptr, x, eps, ACT_SWISH, n->pre_beta, gb.xin, gin, gb.bpart,
+                                nin, GRAD_BLOCKS, s));
         if (gr->dpre_beta) INF_TRY(launch_beta_reduce(gb.bpart, GRAD_BLOCKS, gr->dpre_beta, 0, s));
       } else if (gx) {
         if (G_pri) INF_HIP(hipMemcpyAsync(gx, gb.ga, sizeof(float) * nin, hipMemcpyDeviceToDevice, s));
@@ -3106,6 +3127,90 @@ int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const floa
       }
     }
   }
+  return INF_OK;
+}
+}  // namespace
+
+extern "C" {
+// Gradient of s = sum_b w_b^T J(x_b) eps_b (w fixed) with respect to x and every parameter, and the value s_b per
+// sample (conv nets): the memory-efficient Neumann estimator's surrogate (implicit_block.py:388-394,437-438),
+// forward-over-reverse on the engine.  fc nets: x, w, eps, gx in the (B, d) boundary layout, value NULL.
+int inf_net_surrogate_grad(InfNet* n, const float* x, const float* w, const float* eps, float* value, float* gx,
+                           const InfNetGrads* gr, int B, void* ws, size_t ws_bytes, void* stream) {
+  if (!n || !x || !w || !eps || !gr || B <= 0) return INF_ERR_INVALID;
+  if (!grad_supported(n) || (n->fc && value)) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  GradBufs gb;
+  if (!ws || carve_grad(n, B, ws, ws_bytes, gb) > ws_bytes) return INF_ERR_WORKSPACE;
+  if (!n->fc) return surrogate_core(n, x, w, eps, value, gx, gr, B, gb, s);
+  INF_TRY(launch_transpose(x, gb.x_t, B, n->d, s));
+  INF_TRY(launch_transpose(w, gb.w_t, B, n->d, s));
+  INF_TRY(launch_transpose(eps, gb.e_t, B, n->d, s));
+  INF_TRY(surrogate_core(n, gb.x_t, gb.w_t, gb.e_t, nullptr, gx ? gb.gx_t : nullptr, gr, B, gb, s));
+  if (gx) INF_TRY(launch_transpose(gb.gx_t, gx, n->d, B, s));
+  return INF_OK;
+}
+
+// ---- the log-det estimators' gradients for fc nets (the training path of train_tabular.py / train_toy.py) -----------
+static size_t logdet_grad_layout(InfNet* n, int B, int mode, int n_terms, char* ws, size_t cap, Bufs* bf, GradBufs* gb,
+                                 float** A, float** bv, float** xr, float** gxs, float** eps_t, float** a_scr) {
+  const int T = mode == LOGDET_SERIES ? n_terms : n->d;
+  const long N = (long)T * B;
+  Bufs bf0;
+  GradBufs gb0;
+  const size_t s1 = (carve(n, B, 1, ws, ws ? cap : 0, bf ? *bf : bf0) + 255) & ~(size_t)255;
+  char* w2 = ws ? ws + s1 : nullptr;
+  const size_t s2 = (carve_grad(n, (int)N, w2, ws ? (cap > s1 ? cap - s1 : 0) : 0, gb ? *gb : gb0) + 255) & ~(size_t)255;
+  WS w{ws ? ws + s1 + s2 : nullptr, ws ? (cap > s1 + s2 ? cap - s1 - s2 : 0) : 0, 0};
+  float* p[6];
+  const size_t cnt[6] = {(size_t)n->d * N, (size_t)n->d * N, (size_t)n->d * N, (size_t)n->d * N, (size_t)n->d * B,
+                         mode == LOGDET_SERIES ? (size_t)n_terms * n->d * B : 1};
+  for (int i = 0; i < 6; ++i) p[i] = w.take<float>(cnt[i]);
+  if (A) {
+    *A = p[0];
+    *bv = p[1];
+    *xr = p[2];
+    *gxs = p[3];
+    *eps_t = p[4];
+    *a_scr = p[5];
+  }
+  return s1 + s2 + w.off + 256;
+}
+
+size_t inf_logdet_grad_workspace_bytes(InfNet* n, int B, int mode, int n_terms) {
+  if (!n || B <= 0 || mode < LOGDET_SERIES || mode > LOGDET_TRACE || (mode != LOGDET_EXACT && n_terms < 1)) return 0;
+  return logdet_grad_layout(n, B, mode, n_terms, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, nullptr);
+}
+
+// g . S(x) differentiated into every parameter of an fc net and into x, S_b one of the log-det estimators of a sample
+// (mode INF_LOGDET_SERIES / EXACT / TRACE, pointwise.hip logdet_pairs_kernel): the Jacobian per sample (fc_jacobian),
+// the estimator's bilinear pairs at x, then one forward-over-reverse pass over the T B stacked pairs (surrogate_core:
+// the GEMM chains of the generic path, N = T B columns), the x-gradient summed over each sample's pairs.
+int inf_logdet_grad(InfNet* n, const float* x, int mode, const float* eps, const float* coeff, int n_terms,
+                    const float* gout, float* value, float* gx, const InfNetGrads* gr, int B, void* ws, size_t ws_bytes,
+                    void* stream) {
+  if (!n || !x || !gr || B <= 0 || mode < LOGDET_SERIES || mode > LOGDET_TRACE) return INF_ERR_INVALID;
+  if (mode == LOGDET_SERIES && (!eps || !coeff || n_terms < 1 || n_terms > 128)) return INF_ERR_INVALID;
+  if (mode == LOGDET_TRACE && (!coeff || n_terms < 1 || n_terms > 128)) return INF_ERR_INVALID;
+  if (!n->fc || n->d > 16 || !grad_supported(n)) return INF_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  Bufs bf;
+  GradBufs gb;
+  float *A, *bv, *xr, *gxs, *eps_t, *a_scr;
+  const int nt = mode == LOGDET_EXACT ? 1 : n_terms;
+  if (!ws || logdet_grad_layout(n, B, mode, nt, reinterpret_cast<char*>(ws), ws_bytes, &bf, &gb, &A, &bv, &xr, &gxs,
+                                &eps_t, &a_scr) > ws_bytes)
+    return INF_ERR_WORKSPACE;
+  const int T = mode == LOGDET_SERIES ? n_terms : n->d;
+  const float* tang = nullptr;
+  INF_TRY(fc_jacobian(n, x, B, bf, &tang, s));                     // also leaves x internal in bf.xin
+  if (mode == LOGDET_SERIES) INF_TRY(launch_transpose(eps, eps_t, B, n->d, s));
+  const float one = 1.f;
+  INF_TRY(launch_logdet_pairs(mode, tang, eps_t, bf.xin, gout, mode == LOGDET_EXACT ? &one : coeff, nt, n->d, B, A, bv,
+                              xr, value, a_scr, s));
+  INF_TRY(surrogate_core(n, xr, A, bv, nullptr, gx ? gxs : nullptr, gr, T * B, gb, s));
+  if (gx) INF_TRY(launch_sum_pairs(gxs, T, n->d, B, gx, s));
   return INF_OK;
 }
 

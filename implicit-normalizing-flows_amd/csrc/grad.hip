@@ -485,47 +485,68 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
 // activation algebra.  All tensors (B, C, P) contiguous; per-block fp64 partials of the beta terms
 // (bpart[block]) are reduced by beta_reduce.
 // ------------------------------------------------------------------------------------------------
-// first order:  gprev = ga * s'(h);  beta += ga * ds/dbeta(h)
+// The activation's value and first two derivatives (and, Swish only, the beta terms) at h: Swish (activations.py:64-71)
+// with beta, Sin (activations.py:7-12) sin(2 pi h) / (2 pi), cos(2 pi h), -2 pi sin(2 pi h)
+template <int ACT>
+__device__ __forceinline__ SwishD act_all(float h, float bs, float sb) {
+  if constexpr (ACT == ACT_SWISH) {
+    return swish_all(h, bs, sb);
+  } else {
+    SwishD d;
+    const float sn = sinf(TWO_PI_F * h), cs = cosf(TWO_PI_F * h);
+    d.s = sn * (0.5f / PI_F);
+    d.d1 = cs;
+    d.d2 = -TWO_PI_F * sn;
+    d.db = 0.f;
+    d.d1b = 0.f;
+    return d;
+  }
+}
+
+// first order:  gprev = ga * s'(h);  beta += ga * ds/dbeta(h)  (Swish)
+template <int ACT>
 __global__ __launch_bounds__(256) void act_bwd1_kernel(const float* ga, const float* h, const float* beta,
                                                         float* gprev, double* bpart, long n) {
   __shared__ double red[16];
-  const float bs = softplus_f(*beta), sb = sigmoid_f(*beta);
+  const float bs = ACT == ACT_SWISH ? softplus_f(*beta) : 0.f, sb = ACT == ACT_SWISH ? sigmoid_f(*beta) : 0.f;
   double acc = 0.0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const SwishD d = swish_all(h[i], bs, sb);
+    const SwishD d = act_all<ACT>(h[i], bs, sb);
     gprev[i] = ga[i] * d.d1;
-    acc += (double)ga[i] * (double)d.db;
+    if (ACT == ACT_SWISH) acc += (double)ga[i] * (double)d.db;
   }
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) bpart[blockIdx.x] = t;
 }
 
 // tangent:  adot = s'(h) * hdot  (in place on hdot)
+template <int ACT>
 __global__ void act_tangent_kernel(float* hdot, const float* h, const float* beta, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float bs = softplus_f(*beta);
-  hdot[i] *= swish_d(h[i], bs);
+  if constexpr (ACT == ACT_SWISH) hdot[i] *= swish_d(h[i], softplus_f(*beta));
+  else hdot[i] *= sinact_d(h[i]);
 }
 
 // second order (forward-over-reverse through a = s(h), adot = s'(h) hdot):
 //   gbar_hdot = gbar_adot s'(h)
 //   gbar_h    = gbar_adot hdot s''(h) + gbar_a s'(h)
-//   beta     += gbar_adot hdot ds'/dbeta + gbar_a ds/dbeta
+//   beta     += gbar_adot hdot ds'/dbeta + gbar_a ds/dbeta  (Swish)
 // gbar_a may be null (zero).
+template <int ACT>
 __global__ __launch_bounds__(256) void act_bwd2_kernel(const float* gbar_adot, const float* gbar_a, const float* h,
                                                         const float* hdot, const float* beta, float* gbar_hdot,
                                                         float* gbar_h, double* bpart, long n) {
   __shared__ double red[16];
-  const float bs = softplus_f(*beta), sb = sigmoid_f(*beta);
+  const float bs = ACT == ACT_SWISH ? softplus_f(*beta) : 0.f, sb = ACT == ACT_SWISH ? sigmoid_f(*beta) : 0.f;
   double acc = 0.0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const SwishD d = swish_all(h[i], bs, sb);
+    const SwishD d = act_all<ACT>(h[i], bs, sb);
     const float ga = gbar_adot[i], ha = hdot[i];
     const float gb = gbar_a ? gbar_a[i] : 0.f;
     gbar_hdot[i] = ga * d.d1;
     gbar_h[i] = ga * ha * d.d2 + gb * d.d1;
-    acc += (double)ga * (double)ha * (double)d.d1b + (double)gb * (double)d.db;
+    if (ACT == ACT_SWISH) acc += (double)ga * (double)ha * (double)d.d1b + (double)gb * (double)d.db;
   }
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) bpart[blockIdx.x] = t;
@@ -581,32 +602,47 @@ __global__ void sigma_chain_kernel(const float* dWe, const float* dsig, const fl
   dW[i] = v;
 }
 
-int launch_act_bwd1(const float* ga, const float* h, const float* beta, float* gprev, double* bpart, long n,
+int launch_act_bwd1(const float* ga, const float* h, int act, const float* beta, float* gprev, double* bpart, long n,
                     int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(act_bwd1_kernel, dim3(nblocks), dim3(256), 0, s, ga, h, beta, gprev, bpart, n);
+  if (act == ACT_SWISH)
+    hipLaunchKernelGGL(act_bwd1_kernel<ACT_SWISH>, dim3(nblocks), dim3(256), 0, s, ga, h, beta, gprev, bpart, n);
+  else
+    hipLaunchKernelGGL(act_bwd1_kernel<ACT_SIN>, dim3(nblocks), dim3(256), 0, s, ga, h, beta, gprev, bpart, n);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
-// out = swish(h) (activations.py:64-71), once per element: the weight-gradient operand of a layer whose input
-// is the swish of a stored pre-activation (the wgrad loaders would otherwise recompute it per output tile)
-__global__ void swish_apply_kernel(const float* h, const float* beta, float* out, long n) {
+// out = act(h) (Swish activations.py:64-71, Sin :7-12), once per element: the weight-gradient operand of a layer whose
+// input is the activation of a stored pre-activation (the wgrad loaders would otherwise recompute it per output tile)
+template <int ACT>
+__global__ void act_apply_kernel(const float* h, const float* beta, float* out, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = swish_f(h[i], softplus_f(*beta));
+  if (i >= n) return;
+  if constexpr (ACT == ACT_SWISH) out[i] = swish_f(h[i], softplus_f(*beta));
+  else out[i] = sinact_f(h[i]);
 }
-int launch_swish_apply(const float* h, const float* beta, float* out, long n, hipStream_t s) {
-  hipLaunchKernelGGL(swish_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, h, beta, out, n);
+int launch_act_apply(const float* h, int act, const float* beta, float* out, long n, hipStream_t s) {
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (act == ACT_SWISH) hipLaunchKernelGGL(act_apply_kernel<ACT_SWISH>, g, dim3(256), 0, s, h, beta, out, n);
+  else hipLaunchKernelGGL(act_apply_kernel<ACT_SIN>, g, dim3(256), 0, s, h, beta, out, n);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
-int launch_act_tangent(float* hdot, const float* h, const float* beta, long n, hipStream_t s) {
-  hipLaunchKernelGGL(act_tangent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdot, h, beta, n);
+int launch_act_tangent(float* hdot, const float* h, int act, const float* beta, long n, hipStream_t s) {
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (act == ACT_SWISH) hipLaunchKernelGGL(act_tangent_kernel<ACT_SWISH>, g, dim3(256), 0, s, hdot, h, beta, n);
+  else hipLaunchKernelGGL(act_tangent_kernel<ACT_SIN>, g, dim3(256), 0, s, hdot, h, beta, n);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }
-int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, const float* beta,
-                    float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(act_bwd2_kernel, dim3(nblocks), dim3(256), 0, s, gbar_adot, gbar_a, h, hdot, beta, gbar_hdot,
-                     gbar_h, bpart, n);
+int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, int act,
+                    const float* beta, float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks,
+                    hipStream_t s) {
+  if (act == ACT_SWISH)
+    hipLaunchKernelGGL(act_bwd2_kernel<ACT_SWISH>, dim3(nblocks), dim3(256), 0, s, gbar_adot, gbar_a, h, hdot, beta,
+                       gbar_hdot, gbar_h, bpart, n);
+  else
+    hipLaunchKernelGGL(act_bwd2_kernel<ACT_SIN>, dim3(nblocks), dim3(256), 0, s, gbar_adot, gbar_a, h, hdot, beta,
+                       gbar_hdot, gbar_h, bpart, n);
   INF_CHECK_LAUNCH();
   return INF_OK;
 }

@@ -135,6 +135,12 @@ int launch_permute_k23(const uint16_t* src, uint16_t* dst, long ntiles, hipStrea
 
 // exact small log-det per sample: J[b] = I + T[b] with T stored tangents (d, d, B) feature-major
 int launch_logdet_small(const float* tang, float* out, int d, int batch, long stride_j, hipStream_t s);
+// the log-det estimators' gradients as stacked (A, b) pairs at x (pointwise.hip logdet_pairs_kernel; fc nets, d <= 16)
+enum { LOGDET_SERIES = 0, LOGDET_EXACT = 1, LOGDET_TRACE = 2 };
+int launch_logdet_pairs(int mode, const float* tang, const float* eps, const float* x, const float* gout,
+                        const float* coeff_host, int n_terms, int d, int batch, float* A, float* bv, float* xr,
+                        float* value, float* a_scr, hipStream_t s);
+int launch_sum_pairs(const float* gs, int T, int d, int batch, float* gx, hipStream_t s);
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s);
 // fc layout (d, B): f0 holds d values
@@ -351,12 +357,14 @@ struct WgradArgs {
   int nsplit, max_split;
 };
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
-int launch_act_bwd1(const float* ga, const float* h, const float* beta, float* gprev, double* bpart, long n,
+// activation algebra of the gradient chains (act: ACT_SWISH with beta, or ACT_SIN)
+int launch_act_bwd1(const float* ga, const float* h, int act, const float* beta, float* gprev, double* bpart, long n,
                     int nblocks, hipStream_t s);
-int launch_act_tangent(float* hdot, const float* h, const float* beta, long n, hipStream_t s);
-int launch_swish_apply(const float* h, const float* beta, float* out, long n, hipStream_t s);
-int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, const float* beta,
-                    float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks, hipStream_t s);
+int launch_act_tangent(float* hdot, const float* h, int act, const float* beta, long n, hipStream_t s);
+int launch_act_apply(const float* h, int act, const float* beta, float* out, long n, hipStream_t s);
+int launch_act_bwd2(const float* gbar_adot, const float* gbar_a, const float* h, const float* hdot, int act,
+                    const float* beta, float* gbar_hdot, float* gbar_h, double* bpart, long n, int nblocks,
+                    hipStream_t s);
 int launch_channel_sum(const float* g, int B, int C, int P, float* out, hipStream_t s);
 int launch_beta_reduce(const double* bpart, int n, float* out, int accumulate, hipStream_t s);
 int launch_sigma_chain(const float* dWe, const float* W, const float* dsig, const float* factor, float coeff,

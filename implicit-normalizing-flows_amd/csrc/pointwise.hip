@@ -1131,6 +1131,181 @@ int launch_trace_series(const float* tang, const float* coeff_host, int n_terms,
   return INF_OK;
 }
 
+// ---- the log-det estimators' gradients as pairs (fc nets, engine.hip inf_logdet_grad) -------------------------------
+// Every estimator's differential is a sum of bilinear terms in dJ: d S_b = sum_t A_tb^T dJ(x_b) b_tb (dJ over the
+// parameters and x), so g_b S_b differentiates as the forward-over-reverse surrogate of the stacked pairs.  Per sample
+// (one thread), from its Jacobian J (fc_jacobian's tangent layout) and the upstream gradient g_b:
+//   series  S = sum_k c_k eps^T J^k eps (basic_logdet_estimator, implicit_block.py:418-426; c_k = coeff[k-1]):
+//           d S = sum_k c_k sum_{j+m=k-1} a_j^T dJ b_m with a_j = (J^T)^j eps, b_m = J^m eps, so the n pairs are
+//           A_m = g sum_{j<=n-1-m} c_{j+m+1} a_j, b_m (m < n);
+//   logdet  S = log|det(I + J)| (batch_jacobian + torch.logdet, implicit_block.py:249-260): d S = tr((I + J)^-1 dJ), the
+//           d pairs A_j = g row j of (I + J)^-1, b_j = e_j;
+//   trace   S = sum_k c_k tr(J^k) (exact_trace, :323-343; coeff[0] the bare trace's 1): d S = tr(P dJ),
+//           P = sum_k k c_k J^(k-1), the d pairs A_j = g row j of P, b_j = e_j.
+// Outputs, column t B + b of (d, T B) feature-major arrays: A, bv, and xr = x (the point each pair is taken at); value[b] = S.
+// a_scr: (n, d, B) scratch for the series' left vectors.
+__global__ void logdet_pairs_kernel(int mode, const float* tang, const float* eps, const float* x, const float* gout,
+                                    CoeffTable ct, int n_terms, int d, int batch, float* A, float* bv, float* xr,
+                                    float* value, float* a_scr) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  float J[16][16];
+  const long ld = (long)(d + 1) * batch;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) J[i][j] = tang[i * ld + (j + 1) * (long)batch + b];
+  const float g = gout ? gout[b] : 1.f;
+  const int T = mode == LOGDET_SERIES ? n_terms : d;
+  const long N = (long)T * batch;
+  for (int t = 0; t < T; ++t)
+    for (int i = 0; i < d; ++i) xr[i * N + (long)t * batch + b] = x[(long)i * batch + b];
+  if (mode == LOGDET_SERIES) {
+    float e[16], a[16], v[16], wa[16], wv[16];
+    for (int i = 0; i < d; ++i) e[i] = a[i] = v[i] = eps[(long)i * batch + b];
+    double val = 0.0;
+    for (int m = 0; m < n_terms; ++m) {
+      for (int i = 0; i < d; ++i) {
+        a_scr[((long)m * d + i) * batch + b] = a[i];             // a_m
+        bv[i * N + (long)m * batch + b] = v[i];                  // b_m
+      }
+      for (int i = 0; i < d; ++i) {                             // a_{m+1} = J^T a_m, b_{m+1} = J b_m
+        float sa = 0.f, sv = 0.f;
+        for (int k = 0; k < d; ++k) {
+          sa = fmaf(J[k][i], a[k], sa);
+          sv = fmaf(J[i][k], v[k], sv);
+        }
+        wa[i] = sa;
+        wv[i] = sv;
+      }
+      double dot = 0.0;
+      for (int i = 0; i < d; ++i) {
+        a[i] = wa[i];
+        v[i] = wv[i];
+        dot += (double)a[i] * e[i];                             // eps^T J^(m+1) eps
+      }
+      val += (double)ct.c[m] * dot;
+    }
+    for (int m = 0; m < n_terms; ++m) {
+      float acc[16];
+      for (int i = 0; i < d; ++i) acc[i] = 0.f;
+      for (int j = 0; j + m < n_terms; ++j) {
+        const float c = ct.c[j + m];
+        for (int i = 0; i < d; ++i) acc[i] = fmaf(c, a_scr[((long)j * d + i) * batch + b], acc[i]);
+      }
+      for (int i = 0; i < d; ++i) A[i * N + (long)m * batch + b] = g * acc[i];
+    }
+    if (value) value[b] = (float)val;
+    return;
+  }
+  float P[16][16];
+  double val = 0.0;
+  if (mode == LOGDET_EXACT) {
+    // (I + J)^-1 by Gauss-Jordan with partial pivoting; log|det| from the pivots
+    float M[16][16];
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        M[i][j] = (i == j ? 1.f : 0.f) + J[i][j];
+        P[i][j] = i == j ? 1.f : 0.f;
+      }
+    float logabs = 0.f;
+    int sign = 1;
+    for (int k = 0; k < d; ++k) {
+      int piv = k;
+      float best = fabsf(M[k][k]);
+      for (int i = k + 1; i < d; ++i)
+        if (fabsf(M[i][k]) > best) {
+          best = fabsf(M[i][k]);
+          piv = i;
+        }
+      if (piv != k) {
+        for (int j = 0; j < d; ++j) {
+          float t = M[k][j];
+          M[k][j] = M[piv][j];
+          M[piv][j] = t;
+          t = P[k][j];
+          P[k][j] = P[piv][j];
+          P[piv][j] = t;
+        }
+        sign = -sign;
+      }
+      const float pv = M[k][k];
+      if (pv < 0.f) sign = -sign;
+      logabs += logf(fabsf(pv));
+      const float r = 1.f / pv;
+      for (int j = 0; j < d; ++j) {
+        M[k][j] *= r;
+        P[k][j] *= r;
+      }
+      for (int i = 0; i < d; ++i) {
+        if (i == k) continue;
+        const float f = M[i][k];
+        for (int j = 0; j < d; ++j) {
+          M[i][j] -= f * M[k][j];
+          P[i][j] -= f * P[k][j];
+        }
+      }
+    }
+    val = sign > 0 ? logabs : NAN;
+  } else {
+    // P = sum_k k c_k J^(k-1), val = sum_k c_k tr(J^k)
+    float Q[16][16];                                             // J^(k-1)
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        Q[i][j] = i == j ? 1.f : 0.f;
+        P[i][j] = 0.f;
+      }
+    for (int k = 1; k <= n_terms; ++k) {
+      const float c = ct.c[k - 1];
+      float R[16][16];                                           // J^k = J Q
+      for (int i = 0; i < d; ++i)
+        for (int j = 0; j < d; ++j) {
+          P[i][j] = fmaf((float)k * c, Q[i][j], P[i][j]);
+          float sm = 0.f;
+          for (int q = 0; q < d; ++q) sm = fmaf(J[i][q], Q[q][j], sm);
+          R[i][j] = sm;
+        }
+      double tr = 0.0;
+      for (int i = 0; i < d; ++i) {
+        for (int j = 0; j < d; ++j) Q[i][j] = R[i][j];
+        tr += Q[i][i];
+      }
+      val += (double)c * tr;
+    }
+  }
+  for (int t = 0; t < d; ++t)
+    for (int i = 0; i < d; ++i) {
+      A[i * N + (long)t * batch + b] = g * P[t][i];
+      bv[i * N + (long)t * batch + b] = i == t ? 1.f : 0.f;
+    }
+  if (value) value[b] = (float)val;
+}
+int launch_logdet_pairs(int mode, const float* tang, const float* eps, const float* x, const float* gout,
+                        const float* coeff_host, int n_terms, int d, int batch, float* A, float* bv, float* xr,
+                        float* value, float* a_scr, hipStream_t s) {
+  if (d > 16 || n_terms > 128 || n_terms < 1) return INF_ERR_UNSUPPORTED;
+  CoeffTable ct;
+  for (int k = 0; k < 128; ++k) ct.c[k] = k < n_terms ? coeff_host[k] : 0.f;
+  hipLaunchKernelGGL(logdet_pairs_kernel, dim3((batch + 63) / 64), dim3(64), 0, s, mode, tang, eps, x, gout, ct, n_terms,
+                     d, batch, A, bv, xr, value, a_scr);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+// gx (B, d) boundary layout = sum over the T pairs of the stacked (d, T B) x-gradient
+__global__ void sum_pairs_kernel(const float* gs, int T, int d, int batch, float* gx) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)batch * d) return;
+  const int b = (int)(e / d), i = (int)(e - (long)b * d);
+  const long N = (long)T * batch;
+  float acc = 0.f;
+  for (int t = 0; t < T; ++t) acc += gs[i * N + (long)t * batch + b];
+  gx[e] = acc;
+}
+int launch_sum_pairs(const float* gs, int T, int d, int batch, float* gx, hipStream_t s) {
+  const long n = (long)batch * d;
+  hipLaunchKernelGGL(sum_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gs, T, d, batch, gx);
+  INF_CHECK_LAUNCH();
+  return INF_OK;
+}
+
 // forward-mode activation on [primal | ntang tangent blocks], feature-major (d_out, (1+ntang)*B):
 // primal a -> act(a), tangents t -> act'(a) * t.
 __global__ void fwdmode_act_kernel(float* a, int d_out, int batch, int ntang, int act, const float* beta) {

@@ -147,6 +147,9 @@ _SIGS = {
     'inf_banach_find_root': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                             ctypes.POINTER(ctypes.c_int), _P, ctypes.c_size_t, _P]),
     'inf_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int]),
+    'inf_logdet_grad_workspace_bytes': (ctypes.c_size_t, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    'inf_logdet_grad': (ctypes.c_int, [_P, _P, ctypes.c_int, _P, ctypes.POINTER(ctypes.c_float), ctypes.c_int, _P, _P,
+                                       _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t, _P]),
     'inf_net_param_grad': (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P, ctypes.c_size_t,
                                           _P]),
     'inf_net_surrogate_grad': (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(NetGrads), ctypes.c_int, _P,

@@ -207,6 +207,63 @@ class _MemEffNeumannNative(torch.autograd.Function):
         return (gx * dL, None, None, None, None) + tuple(g * dL if g is not None else None for g in ctx.grads)
 
 
+def _logdet_value(native, x, mode, eps, coeff):
+    """S_b of one fc net's log-det estimator on the engine (no gradients): the value half of _LogdetFc."""
+    lib = _hip.load()
+    B = x.shape[0]
+    out = torch.empty(B, device=x.device)
+    stream = _hip.stream_of(x)
+    ws = _hip.workspace(x.device, native.ws_bytes(B))
+    xc = x.contiguous()
+    if mode == netgrad.LOGDET_EXACT:
+        _hip.check(lib.inf_logdet_exact(native.handle, _hip.ptr(xc), _hip.ptr(out), B, _hip.ptr(ws), ws.numel(),
+                                        stream), 'inf_logdet_exact')
+        return out
+    carr = coeff.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    if mode == netgrad.LOGDET_TRACE:
+        _hip.check(lib.inf_logdet_exact_trace(native.handle, _hip.ptr(xc), carr, len(coeff), _hip.ptr(out), B,
+                                              _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_exact_trace')
+        return out
+    _hip.check(lib.inf_logdet_series(native.handle, _hip.ptr(xc), _hip.ptr(eps.contiguous()), carr, len(coeff),
+                                     _hip.ptr(out), B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series')
+    return out
+
+
+class _LogdetFc(torch.autograd.Function):
+    """A log-det estimator of one fc net with its gradients on the engine: the basic power series with the graph
+    (implicit_block.py:418-426, create_graph=True), the brute-force log|det(I + J)| (:249-260) and the exact-trace series
+    (:323-343), as autograd would differentiate them.  Forward: S_b (engine value paths); backward: inf_logdet_grad with
+    the incoming per-sample gradient (parameters and x).  mem_eff: MemoryEfficientLogDetEstimator (:373-415) -- the
+    gradients taken in the forward pass for a unit gradient, scaled by the incoming gradient's first element."""
+
+    @staticmethod
+    def forward(ctx, x, native, module, mode, eps, coeff, mem_eff, *params):
+        xd = x.detach()
+        ctx.native, ctx.module, ctx.mode, ctx.eps, ctx.coeff, ctx.mem_eff = native, module, mode, eps, coeff, mem_eff
+        if mem_eff:
+            value, grads, gx = _engine_result(
+                netgrad.logdet_grads(native, module, xd, mode, eps, coeff, torch.ones(x.shape[0], device=x.device)),
+                module, 'inf_logdet_grad')
+            ctx.grads = [grads.get(p) for p in params]
+            ctx.save_for_backward(gx)
+            return value
+        ctx.save_for_backward(xd)
+        ctx.params = params
+        return _logdet_value(native, xd, mode, eps, coeff)
+
+    @staticmethod
+    def backward(ctx, g):
+        none = (None,) * 6
+        if ctx.mem_eff:
+            gx, = ctx.saved_tensors
+            dL = g[0].detach()
+            return (gx * dL,) + none + tuple(t * dL if t is not None else None for t in ctx.grads)
+        xd, = ctx.saved_tensors
+        _, grads, gx = _engine_result(netgrad.logdet_grads(ctx.native, ctx.module, xd, ctx.mode, ctx.eps, ctx.coeff,
+                                                           g.detach().contiguous()), ctx.module, 'inf_logdet_grad')
+        return (gx,) + none + tuple(grads.get(p) for p in ctx.params)
+
+
 class RootFind:
     """RootFind.apply(nnet_z, nnet_x, z0, x, method, eps, threshold) (implicit_block.py:51-100): the root z of
     z + nnet_z(z) = x + nnet_x(x), by 'broyden' (from 0, Banach fallback on prot_break; inf_root_find) or 'banach'
@@ -465,7 +522,15 @@ class imBlock(nn.Module):
         """_logdetgrad with gradients (implicit_block.py:245-350).  The n-term Neumann series runs on the
         engine (inf_neumann_vector); the surrogate w^T J eps and its parameter gradients go through
         autograd on the nets."""
+        engine = self._engine_grads(x)
         if (self.brute_force or not self.training) and x.dim() == 2 and x.shape[1] <= 10:
+            if engine:                   # log|det(I + J)| and its gradients on the engine
+                nx, nz, stream = self._native(x)
+                lx = _LogdetFc.apply(x, nx, self.nnet_x, netgrad.LOGDET_EXACT, None, None, False,
+                                     *list(self.nnet_x.parameters()))
+                lz = _LogdetFc.apply(z, nz, self.nnet_z, netgrad.LOGDET_EXACT, None, None, False,
+                                     *list(self.nnet_z.parameters()))
+                return (lx - lz).view(-1, 1)
             xg = x if x.requires_grad else x.detach().requires_grad_(True)
             zg = z if z.requires_grad else z.detach().requires_grad_(True)
             with torch.enable_grad():
@@ -473,6 +538,14 @@ class imBlock(nn.Module):
                 Jz = solvers.batch_jacobian(zg + self.nnet_z(zg), zg)
                 return (torch.logdet(Jx) - torch.logdet(Jz)).view(-1, 1)
         n_ps, coeff_fn, ns = self._series_plan()
+        if self.exact_trace and engine:  # the exact-trace series and its gradients on the engine (coeff[0]: bare trace)
+            co = np.array([1.] + [(-1) ** (k + 1) / k * coeff_fn(k) for k in range(2, n_ps + 1)], dtype=np.float32)
+            nx, nz, stream = self._native(x)
+            lx = _LogdetFc.apply(x, nx, self.nnet_x, netgrad.LOGDET_TRACE, None, co, False,
+                                 *list(self.nnet_x.parameters()))
+            lz = _LogdetFc.apply(z, nz, self.nnet_z, netgrad.LOGDET_TRACE, None, co, False,
+                                 *list(self.nnet_z.parameters()))
+            return self._finish_logdet(lx - lz, n_ps, ns)
         if self.exact_trace:
             with torch.enable_grad():
                 out = []
@@ -491,13 +564,17 @@ class imBlock(nn.Module):
         neumann = self.training and self.neumann_grad
         nx, nz, stream = self._native(x)
         ests = []
-        engine = self._engine_grads(x)
         native_neumann = neumann and engine and self.training and self.grad_in_forward
         if native_neumann:        # both branches' Neumann vectors in lockstep (one fused launch per term)
             ws_pair = self._neumann_pair(nx, x.detach(), vareps_x, nz, z.detach(), vareps_z, n_ps, coeff_fn, stream)
         for i, (net, native, t, eps) in enumerate(((self.nnet_x, nx, x, vareps_x), (self.nnet_z, nz, z, vareps_z))):
             if native_neumann:
                 ests.append(_MemEffNeumannNative.apply(t, native, net, ws_pair[i], eps, *list(net.parameters())))
+                continue
+            if not neumann and engine and t.dim() == 2:      # fc nets: the basic series with the graph, engine
+                co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+                ests.append(_LogdetFc.apply(t, native, net, netgrad.LOGDET_SERIES, eps, co,
+                                            bool(self.training and self.grad_in_forward), *list(net.parameters())))
                 continue
             if neumann:
                 w = self._neumann_vector(native, t.detach(), eps, n_ps, coeff_fn, stream)
@@ -514,19 +591,20 @@ class imBlock(nn.Module):
         return self._finish_logdet(ests[0] - ests[1], n_ps, ns)
 
     def _engine_grads(self, t):
-        """Whether the engine computes the parameter gradients of both nets (conv nets with swish
-        activations); otherwise the training graph keeps autograd on the nets."""
-        if t.dim() != 4:
+        """Whether the engine computes the parameter gradients of both nets: conv nets with Swish activations, fc nets
+        (d <= 16) with Swish / Sin; otherwise the training graph keeps autograd on the nets.  (The fc nets' Neumann
+        estimator keeps autograd for its surrogate.)"""
+        if t.dim() not in (2, 4) or (t.dim() == 2 and t.shape[1] > 16):
             return False
-        key = '_engine_grads_ok'
+        key = '_engine_grads_ok' if t.dim() == 4 else '_engine_grads_ok_fc'
         if key not in self.__dict__:
+            allowed = ('InducedNormConv2d', 'Swish') if t.dim() == 4 else ('InducedNormLinear', 'Swish', 'Sin')
             ok = True
             for net in (self.nnet_x, self.nnet_z):
                 for m in net.modules():
                     if isinstance(m, nn.Sequential):
                         continue
-                    name = type(m).__name__
-                    if name not in ('InducedNormConv2d', 'Swish'):
+                    if type(m).__name__ not in allowed:
                         ok = False
             self.__dict__[key] = ok
         return self.__dict__[key]

@@ -4,10 +4,13 @@
                     (implicit_block.py:226-227), ``inf_net_param_grad``
 ``surrogate_grads`` s_b = w_b^T J(x_b) eps_b and d/dx, d/dtheta of sum_b s_b: the memory-efficient
                     Neumann estimator (implicit_block.py:373-415,437-438), ``inf_net_surrogate_grad``
+``logdet_grads``    g . S(x) differentiated into x and every parameter, S one of the log-det estimators of an fc
+                    net (the basic power series with the graph, implicit_block.py:418-426; the brute-force
+                    log|det(I + J)|, :249-260; the exact-trace series, :323-343), ``inf_logdet_grad``
 
 Weight gradients are with respect to the RAW weights (through the Lipschitz normalisation, like
-autograd through ``compute_weight(update=False)``).  Conv nets with swish activations; other nets
-return None and the caller keeps autograd.
+autograd through ``compute_weight(update=False)``).  Conv nets with Swish activations and fc nets with Swish / Sin;
+other nets return None and the caller keeps autograd.
 """
 import ctypes
 
@@ -15,7 +18,9 @@ import torch
 
 from .. import _hip
 
-__all__ = ['param_grads', 'surrogate_grads']
+__all__ = ['param_grads', 'surrogate_grads', 'logdet_grads', 'LOGDET_SERIES', 'LOGDET_EXACT', 'LOGDET_TRACE']
+
+LOGDET_SERIES, LOGDET_EXACT, LOGDET_TRACE = 0, 1, 2     # InfLogdetMode (include/inflow.h)
 
 
 def _slots(module):
@@ -89,4 +94,25 @@ def surrogate_grads(native, module, x, w, eps):
     if rc == _hip.INF_ERR_UNSUPPORTED:
         return None
     _hip.check(rc, 'inf_net_surrogate_grad')
+    return value, grads, gx
+
+
+def logdet_grads(native, module, x, mode, eps, coeff, gout):
+    """-> (S (B,), {param: grad}, grad_x): S_b the estimator at x_b, the gradients of sum_b gout_b S_b; None when the
+    engine does not cover this net.  coeff: the per-term multipliers (series / trace), a float32 numpy array."""
+    lib = _hip.load()
+    B = x.shape[0]
+    ng, keep, grads = _alloc(module)
+    gx = torch.empty_like(x)
+    value = torch.empty(B, device=x.device)
+    n_terms = int(len(coeff)) if coeff is not None else 1
+    ws = _hip.workspace(x.device, lib.inf_logdet_grad_workspace_bytes(native.handle, B, mode, n_terms))
+    carr = coeff.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if coeff is not None else None
+    rc = lib.inf_logdet_grad(native.handle, _hip.ptr(x.contiguous()), mode,
+                             _hip.ptr(eps.contiguous()) if eps is not None else None, carr, n_terms,
+                             _hip.ptr(gout.contiguous()), _hip.ptr(value), _hip.ptr(gx), ctypes.byref(ng), B,
+                             _hip.ptr(ws), ws.numel(), _hip.stream_of(x))
+    if rc == _hip.INF_ERR_UNSUPPORTED:
+        return None
+    _hip.check(rc, 'inf_logdet_grad')
     return value, grads, gx

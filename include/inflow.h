@@ -357,17 +357,34 @@ typedef struct InfNetGrads {
 } InfNetGrads;
 size_t inf_grad_workspace_bytes(InfNet* net, int batch);
 /* d/dtheta sum(gout * nnet(x)) and d/dx (gx may be NULL): the recompute graph's backward
- * (z = f_x(x0) - f_z(z*) + x0, implicit_block.py:226-227). */
+ * (z = f_x(x0) - f_z(z*) + x0, implicit_block.py:226-227).  Conv nets with Swish; fc nets with Swish / Sin (x, gout,
+ * gx in the (B, d) boundary layout). */
 int inf_net_param_grad(InfNet* net, const float* x, const float* gout, float* gx, const InfNetGrads* grads,
                        int batch, void* ws, size_t ws_bytes, void* stream);
 /* s_b = w_b^T J(x_b) eps_b (w fixed): value[b] (may be NULL) and d/dx, d/dtheta of sum_b s_b -- the
- * memory-efficient Neumann estimator's surrogate and its gradients (implicit_block.py:388-394,437-438). */
+ * memory-efficient Neumann estimator's surrogate and its gradients (implicit_block.py:388-394,437-438).  fc nets:
+ * (B, d) boundary layout, value must be NULL. */
 int inf_net_surrogate_grad(InfNet* net, const float* x, const float* w, const float* eps, float* value, float* gx,
                            const InfNetGrads* grads, int batch, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);
+
+/* Gradients of the log-det estimators of an fc net (the training path of train_tabular.py / train_toy.py: the basic
+ * power series with create_graph, implicit_block.py:418-426; the brute-force log|det(I + J)|, :249-260; the exact-trace
+ * series, :323-343): sum_b gout[b] S_b(x_b) differentiated into every parameter (grads, as inf_net_param_grad) and x
+ * (gx, (B, d), nullable); value (B, nullable) receives S_b.  mode:
+ *   INF_LOGDET_SERIES  S_b = sum_k coeff[k-1] eps_b^T J^k eps_b, k = 1..n_terms (coeff[k-1] = (-1)^(k+1)/k coeff_fn(k));
+ *   INF_LOGDET_EXACT   S_b = log|det(I + J(x_b))| (eps, coeff, n_terms unused);
+ *   INF_LOGDET_TRACE   S_b = sum_k coeff[k-1] tr(J^k) (coeff[0] = 1: the bare trace).
+ * x, eps (B, d) boundary layout; coeff a host array.  fc nets with Swish / Sin, d <= 16.
+ * ws >= inf_logdet_grad_workspace_bytes(net, batch, mode, n_terms). */
+typedef enum InfLogdetMode { INF_LOGDET_SERIES = 0, INF_LOGDET_EXACT = 1, INF_LOGDET_TRACE = 2 } InfLogdetMode;
+size_t inf_logdet_grad_workspace_bytes(InfNet* net, int batch, int mode, int n_terms);
+int inf_logdet_grad(InfNet* net, const float* x, int mode, const float* eps, const float* coeff, int n_terms,
+                    const float* gout, float* value, float* gx, const InfNetGrads* grads, int batch, void* ws,
+                    size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -76,11 +76,27 @@ def test_training_gradients_match_reference(golden_dir, name, arch):
     set_probe_mode('reference')
     np.random.seed(int(g['seed']))
     torch.manual_seed(int(g['seed']))
-    if arch['kind'] == 'conv':
-        loss, logpx, z = image_bits_per_dim_graph(m, x, arch['nvals'])
-    else:
-        loss, logpx, z = tabular_nats_graph(m, x)
-    loss.backward()
+    # every torch forward of a net layer during the step is recorded (there should be none: the engine runs them)
+    from lib.layers.base import lipschitz_ops as lo
+    calls = []
+    real = {c: c.forward for c in (lo.InducedNormLinear, lo.InducedNormConv2d)}
+
+    def spy(cls):
+        def fwd(self, *a, **k):
+            calls.append(cls.__name__)
+            return real[cls](self, *a, **k)
+        return fwd
+    try:
+        for c in real:
+            c.forward = spy(c)
+        if arch['kind'] == 'conv':
+            loss, logpx, z = image_bits_per_dim_graph(m, x, arch['nvals'])
+        else:
+            loss, logpx, z = tabular_nats_graph(m, x)
+        loss.backward()
+    finally:
+        for c, f in real.items():
+            c.forward = f
     torch.cuda.synchronize()
     blocks = imblocks(m)
     for i, b in enumerate(blocks):
@@ -91,8 +107,11 @@ def test_training_gradients_match_reference(golden_dir, name, arch):
         if arch['kind'] == 'conv':
             assert b.last_broyden_backward['nstep'] == int(g['b%d_bwd_nstep' % i]), 'block %d bwd nstep' % i
     assert abs(loss.item() - float(g['loss'])) <= 1e-5, (loss.item(), float(g['loss']))
-    if arch['kind'] == 'conv':       # the engine computed the parameter gradients (no autograd on the nets)
-        assert all(b.__dict__.get('_engine_grads_ok') for b in blocks)
+    # the engine computed the parameter gradients (no autograd on the nets): conv nets, and fc nets (the recompute, the
+    # basic series with the graph / the brute-force log-det, inf_logdet_grad)
+    key = '_engine_grads_ok' if arch['kind'] == 'conv' else '_engine_grads_ok_fc'
+    assert all(b.__dict__.get(key) for b in blocks)
+    assert not calls, 'a net module ran its torch forward in the training step: %s' % calls[:3]
     n = _check_grads(m, g)
     assert n == len([k for k in g.files if k.startswith('g:') or k.startswith('gs:')])
 
