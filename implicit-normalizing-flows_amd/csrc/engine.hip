@@ -125,6 +125,7 @@ struct InfNet {
   int convergence = INF_CONV_GLOBAL;   // INF_OPT_CONVERGENCE (read on the solved net)
   int line_search = 0;                 // INF_OPT_LINE_SEARCH (read on the solved net)
   int exact_scale = 0;     // INF_OPT_K128_EXACT_SCALE
+  int presplit = 1;        // INF_OPT_FUSED_PRESPLIT
   int fc_block = 1;        // INF_OPT_FC_BLOCK (read on net_z of inf_imblock_eval_exact)
   int fc_series = 1;       // INF_OPT_FC_SERIES (read on the first net of inf_logdet_series[_pair])
   // fused fc path (fcnet.hip): the whole net in one launch per evaluation (forward and forward-mode Jacobian)
@@ -185,6 +186,7 @@ struct Bufs {
   // (OutArgs::stop_ev) when its launcher can, which sets stop_bound; enqueue_sumsq then records no marker after it
   hipEvent_t stop_ev = nullptr;
   bool stop_bound = false;
+  bool sample_sums = false;   // conv residuals write each sample's total into bf.part (the readback slot; broyden_core)
 };
 
 size_t per_sample_hidden(const InfNet* n) { return (size_t)n->hidden_max * (n->fc ? 1 : n->P); }
@@ -315,6 +317,7 @@ Net313Args net313_args(const InfNet* n, const float* in, int B, Bufs& bf, bool v
   f.seg = n->W < 64 ? n->W : 64;
   f.k128 = n->k128;
   f.exact_scale = n->exact_scale;
+  f.presplit = n->presplit;
   return f;
 }
 
@@ -501,7 +504,7 @@ int enqueue_sumsq(InfNet* f, int B, Bufs& bf, SumsSlot* sl, hipStream_t s, const
   // fc nets write one partial per sample: with the global rule those are the sums already (0 + x == x for the
   // non-negative or NaN sums), so the readback takes them directly and the reduction launch is skipped
   const bool ps_on = ps && ps->on;
-  const bool direct = f->fc && !ps_on;
+  const bool direct = (f->fc || bf.sample_sums) && !ps_on;
   if (direct && bf.part == sl->host) {               // the residual launch wrote the sums into the slot itself
     const bool bound = bf.stop_bound && bf.stop_ev == sl->ev;
     bf.stop_bound = false;
@@ -582,6 +585,7 @@ int eval_resid_part(InfNet* f, const float* z, const float* zsub, const float* x
   a.out2 = bf.fcur;
   a.partial = bf.part;
   a.nchunk = bf.nchunk;
+  a.sample_sums = bf.sample_sums;
   a.stop_ev = bf.stop_ev;
   a.stop_bound = &bf.stop_bound;
   return run_forward(f, z, B, bf, OM_RESID, &a, s);
@@ -679,9 +683,14 @@ static int ps_collect(Bufs& bf, int B, int T, InfBroydenStats& stats, std::vecto
 // sample against eps sqrt(d) (the reference's result for a batch of one, i.e. independent of how the batch is
 // sharded), with the decisions taken on the device (ps_decide_kernel) and stopped samples frozen.
 // stats.sample_* (host arrays, nullable) receive the per-sample outcome in that mode.
+#ifndef SAMPLE_SUMS
+#define SAMPLE_SUMS 1   // 0: conv residuals write chunk partials and a reduction launch sums them (A/B builds)
+#endif
+
 int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, InfBroydenStats& stats,
                  std::vector<double>& lowest_ss, Bufs& bf, hipStream_t s, bool keep_f = false,
-                 const StepFn* step_fn = nullptr, const StartFn* start_fn = nullptr, SpecTail* tail = nullptr) {
+                 const StepFn* step_fn = nullptr, const StartFn* start_fn = nullptr, SpecTail* tail = nullptr,
+                 bool resid_sample_sums = false) {
   const size_t E = (size_t)B * f->d;
   const long cs = (long)E;
   const long sb = f->fc ? 1 : f->d, si = f->fc ? B : 1;
@@ -742,7 +751,11 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
   // zero-copy readback (fc nets, global rule): each residual launch writes its per-sample sums straight into the
   // pinned slot its norm is read from (bf.part points there while it is enqueued), so no copy launch sits between
   // the residual and the event the host waits on; bf.part is restored on every return path
-  const bool zc = f->fc && !per_sample;
+  // conv nets whose residual launches can write per-sample totals (resid_sample_sums: the root solve's
+  // eval_resid_part / resid_bcast, d <= 4 residual chunks per sample): the residual launch itself sums each sample
+  // over its chunks (one block per sample, conv_out_resid_sample_kernel) into the slot, so no reduction launch sits
+  // between it and the readback either.  (The implicit backward's residual writes chunk partials: not here.)
+  const bool zc = (f->fc || (resid_sample_sums && SAMPLE_SUMS && out_nchunk(f->d) <= 4)) && !per_sample;
   struct PartRestore {
     Bufs& b;
     double* p;
@@ -751,12 +764,14 @@ int broyden_core(InfNet* f, const ResidFn& resid, int B, int T, double eps_in, I
       b.part = p;
       b.stop_ev = e;
       b.stop_bound = false;
+      b.sample_sums = false;
     }
   } part_restore{bf, bf.part, bf.stop_ev};
   auto target = [&](SumsSlot* sl) {
     if (zc) {
       bf.part = sl->host;
       bf.stop_ev = sl->ev;
+      bf.sample_sums = !f->fc;
     }
   };
   target(slot[0]);
@@ -1248,7 +1263,8 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     if (first) {
       first = false;
       if (f->fc) return launch_resid_bcast_fc(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, s);
-      return launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s);
+      return launch_resid_bcast(f->f0, bf.xemb, x, gout, bf.fcur, bf.part, B, f->d, bf.nchunk, s, bf.sample_sums,
+                                bf.stop_ev, &bf.stop_bound);
     }
     return eval_resid_part(f, x, x, bf.xemb, gout, dg, gprev, B, bf, s);
   };
@@ -1285,7 +1301,7 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
     INF_TRY(broyden_core_ls(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
   } else {
     INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
-                         f->fc ? &start : nullptr, tail));
+                         f->fc ? &start : nullptr, tail, /*resid_sample_sums=*/true));
   }
   if (diff_detail) {
     std::vector<float> dd(B);
@@ -1869,7 +1885,8 @@ int inf_net_create(const InfNetDesc* desc, InfNet** out) {
                            {"INFLOW_EVAL_OVERLAP", &n->eval_overlap, bin_v, 2},
                            {"INFLOW_CONVERGENCE", &n->convergence, conv_v, 2},
                            {"INFLOW_FC_BLOCK", &n->fc_block, k128_v, 3},
-                           {"INFLOW_FC_SERIES", &n->fc_series, bin_v, 2}};
+                           {"INFLOW_FC_SERIES", &n->fc_series, bin_v, 2},
+                           {"INFLOW_FUSED_PRESPLIT", &n->presplit, bin_v, 2}};
     for (const EnvOpt& o : opts) {
       const char* e = getenv(o.name);
       if (!e || !*e) continue;
@@ -3234,6 +3251,7 @@ int inf_net_set_option(InfNet* n, int option, int value) {
     case INF_OPT_K128_EXACT_SCALE: slot = &n->exact_scale; hi = 1; break;
     case INF_OPT_FC_BLOCK: slot = &n->fc_block; hi = 2; break;
     case INF_OPT_FC_SERIES: slot = &n->fc_series; hi = 1; break;
+    case INF_OPT_FUSED_PRESPLIT: slot = &n->presplit; hi = 1; break;
     default: return -INF_ERR_INVALID;
   }
   if (value < lo || value > hi) return -INF_ERR_INVALID;
@@ -3254,6 +3272,7 @@ int inf_net_get_option(const InfNet* n, int option) {
     case INF_OPT_K128_EXACT_SCALE: return n->exact_scale;
     case INF_OPT_FC_BLOCK: return n->fc_block;
     case INF_OPT_FC_SERIES: return n->fc_series;
+    case INF_OPT_FUSED_PRESPLIT: return n->presplit;
     default: return -INF_ERR_INVALID;
   }
 }

@@ -84,6 +84,22 @@ __device__ __forceinline__ f32x16 mma(const u32x4 (&a)[NP], const u32x4 (&b)[NP]
   if constexpr (NP == 3) return mfma_x6(a, b[0], b[1], b[2], c);
   else return mfma_h3(a, b[0], b[1], c);
 }
+// Pre-split wide kernel, per phase (round 6, same-box A/B of the s2 VJP per step): phase A's im2col
+// planes 2.70 -> 2.53 ms (kept); phase C's operand planes 2.69 (neutral alone); phase B's operand planes 3.26 (slower:
+// the per-wave split of phase B is VALU the weight-stream-bound loop hides under its MFMAs, and the planes cost a put
+// and a barrier), so phase B keeps the per-wave split
+#ifndef PS_A
+#define PS_A 1
+#endif
+#ifndef PS_B
+#define PS_B 0
+#endif
+#ifndef PS_C
+#define PS_C 1
+#endif
+#ifndef PSD
+#define PSD 4        // pre-split wide kernel: weight-fragment ring depth (K tiles) of phases A and B
+#endif
 #ifndef H3_AC
 #define H3_AC 1      // INF_MFMA_F16X3: phases A and C in h3 too (0: x6 there)
 #endif
@@ -104,9 +120,9 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   constexpr int HID = NW * 32 * TM;
   constexpr int NB = F_BN / 32;                     // 32-pixel column tiles per wave
   // two independent nets (the x- and z-branch of an imBlock) can share one launch
-  const int sel = (int)blockIdx.x >= pr.nb0 ? 1 : 0;
+  int sel;
+  const int bid = pair_tile(pr, (int)blockIdx.x, sel);
   const Net313Args& a = pr.a[sel];
-  const int bid = (int)blockIdx.x - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[F_LDS_FLOATS];
 #define STAMP(i_)                                                                            \
   do {                                                                                       \
@@ -141,6 +157,36 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   float* t = smem;                                  // [HID][F_BN] activation tile
   int* koff = reinterpret_cast<int*>(smem + HID * F_BN);   // [K1pad] im2col offsets into vh
   float* vh = smem + HID * F_BN + a.K1pad;          // [C][RH][CW] halo tile + rows*CW zeros
+  // Pre-split B operands (the wide 32-pixel variant in h3, INF_OPT_FUSED_PRESPLIT): every phase's B operand is split
+  // into its fp16 (h, l) planes once, by the threads that produce it, in the MFMA B-fragment order
+  // [(K tile * NB + column block) * 2 + plane][64 lanes] x 16 B, instead of by each of the 8 waves that consume it.
+  // Phase A's im2col planes sit below the column maxima (when they fit); phases B and C's in the activation tile's
+  // space (the same 4 bytes per element as the fp32 tile).  Same scales, same rounding: bitwise the same results.
+  constexpr bool PS = H3AC && F_LDS_FLOATS == LDS_FULL && F_BN == 32 && NW == 8;
+  const bool ps = PS && !(pr.dbg & 32);
+  const int psa_floats = a.K1pad * 32 * NB;
+  u32x4* const pa = reinterpret_cast<u32x4*>(smem + F_LDS_FLOATS - 32 - NW * F_BN - psa_floats);
+  const bool psb = PS_B && ps, psc = PS_C && ps;    // (per-phase build switches: bisecting A/B builds)
+  const bool psa = PS_A && ps && HID * F_BN + a.K1pad + vhz <= F_LDS_FLOATS - 32 - NW * F_BN - psa_floats;
+  u32x4* const tpl = reinterpret_cast<u32x4*>(t);
+  // this lane's four values of accumulator group g (rows 8 g + 4 lh + q of row block rb, column block b) into the
+  // planes: K tile 2 rb + (g >> 1), consumer lane 32 (g & 1) + li, k-slots 4 lh + q (one ds_write_b64 per plane)
+  auto put_planes = [&](u32x4* base, int rb, int b, const f32x16& v, float S) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const _Float16 h0 = (_Float16)(v[4 * g] * S), h1 = (_Float16)(v[4 * g + 1] * S);
+      const _Float16 h2 = (_Float16)(v[4 * g + 2] * S), h3 = (_Float16)(v[4 * g + 3] * S);
+      const _Float16 l0 = (_Float16)__builtin_fmaf(v[4 * g], S, -(float)h0);
+      const _Float16 l1 = (_Float16)__builtin_fmaf(v[4 * g + 1], S, -(float)h1);
+      const _Float16 l2 = (_Float16)__builtin_fmaf(v[4 * g + 2], S, -(float)h2);
+      const _Float16 l3 = (_Float16)__builtin_fmaf(v[4 * g + 3], S, -(float)h3);
+      const f16x2 p0 = {h0, h1}, p1 = {h2, h3}, q0 = {l0, l1}, q1 = {l2, l3};
+      const int kt = 2 * rb + (g >> 1);
+      const int o = ((kt * NB + b) * 2) * 64 + 32 * (g & 1) + li;
+      reinterpret_cast<uint2*>(base + o)[lh] = make_uint2(__builtin_bit_cast(unsigned, p0), __builtin_bit_cast(unsigned, p1));
+      reinterpret_cast<uint2*>(base + o + 64)[lh] = make_uint2(__builtin_bit_cast(unsigned, q0), __builtin_bit_cast(unsigned, q1));
+    }
+  };
 
   // split path: phase A's first operand tile is requested before the staging loads (it is an L2 hit and
   // retires long before the staging data, so it costs the staging nothing and phase A starts without a wait)
@@ -353,66 +399,127 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       eA = -(sc + ldc(a.Ah_exp));
     }
     auto ld3 = [&](int m, int kt, u32x4 (&o)[NPAC]) { ldw<NPAC>(A1w, (long)(rbw + m) * nkt + kt, lane, o); };
-    // B operand (im2col gather from the halo tile) one K tile ahead: its LDS reads and split overlap
-    // this tile's MFMAs
-    auto gath = [&](int kt, float (&x)[NB][8]) {
-      const int* kp = koff + kt * 16 + lh * 8;
-      const int4 k0 = *reinterpret_cast<const int4*>(kp);
-      const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
-      const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+    auto gather_path = [&]() {
+      // B operand (im2col gather from the halo tile) one K tile ahead: its LDS reads and split overlap
+      // this tile's MFMAs
+      auto gath = [&](int kt, float (&x)[NB][8]) {
+        const int* kp = koff + kt * 16 + lh * 8;
+        const int4 k0 = *reinterpret_cast<const int4*>(kp);
+        const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);
+        const int ko[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) x[b][kk] = vh[ko[kk] + pix[b]];
+          for (int kk = 0; kk < 8; ++kk) x[b][kk] = vh[ko[kk] + pix[b]];
+      };
+      // (the 128-VGPR variant gathers and splits in place)
+      u32x4 bq[NB][NPAC];
+      if constexpr (PRE_A) {
+        float x0[NB][8];
+        gath(0, x0);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) splitb<NPAC>(x0[b], sA, bq[b]);
+      }
+      auto tileA = [&](int kt, const u32x4 (&af)[TM][NPAC]) {
+        float xn[NB][8];
+        if constexpr (PRE_A) {
+          gath(min(kt + 1, nkt - 1), xn);
+        } else {
+          gath(kt, xn);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
+        }
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[m][b] = mma<NPAC>(af[m], bq[b], acc[m][b]);
+        if constexpr (PRE_A) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
+        }
+      };
+      u32x4 a0[TM][NPAC], a1[TM][NPAC];
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        if constexpr (PRE_A) {
+#pragma unroll
+          for (int p3 = 0; p3 < NPAC; ++p3) a0[m][p3] = pa0[m][p3];
+        } else {
+          ld3(m, 0, a0[m]);
+        }
+      }
+      for (int kt = 0; kt < nkt; kt += 2) {
+        const bool has1 = kt + 1 < nkt;
+        if (has1) {
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ld3(m, kt + 1, a1[m]);
+        }
+        tileA(kt, a0);
+        if (kt + 2 < nkt) {
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
+        }
+        if (has1) tileA(kt + 1, a1);
+      }
     };
-    // (the 128-VGPR variant gathers and splits in place)
-    u32x4 bq[NB][NPAC];
-    if constexpr (PRE_A) {
-      float x0[NB][8];
-      gath(0, x0);
+    if constexpr (PS) {
+      if (psa) {
+        // the im2col planes, once per workgroup (every wave's phase A reads them with two ds_read_b128 per K tile
+        // and column block instead of 8 gathered ds_read_b32 and the split)
+        for (int s_ = tid; s_ < nkt * 64 * NB; s_ += NT) {
+          const int kt = s_ / (64 * NB), rem = s_ - kt * (64 * NB), b = rem >> 6, ln = rem & 63;
+          const int n = b * 32 + (ln & 31), py = n / seg;
+          const int px_ = py * CW + (n - py * seg);
+          const int* kp = koff + kt * 16 + (ln >> 5) * 8;
+          float x[8];
 #pragma unroll
-      for (int b = 0; b < NB; ++b) splitb<NPAC>(x0[b], sA, bq[b]);
-    }
-    auto tileA = [&](int kt, const u32x4 (&af)[TM][NPAC]) {
-      float xn[NB][8];
-      if constexpr (PRE_A) {
-        gath(min(kt + 1, nkt - 1), xn);
+          for (int kk = 0; kk < 8; ++kk) x[kk] = vh[kp[kk] + px_];
+          u32x4 h, l;
+          split2h(x, sA, h, l);
+          pa[((kt * NB + b) * 2) * 64 + ln] = h;
+          pa[((kt * NB + b) * 2 + 1) * 64 + ln] = l;
+        }
+        __syncthreads();
+        auto tileP = [&](int kt, const u32x4 (&af)[TM][NPAC]) {
+          u32x4 o[NB][2];
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            o[b][0] = pa[((kt * NB + b) * 2) * 64 + lane];
+            o[b][1] = pa[((kt * NB + b) * 2 + 1) * 64 + lane];
+          }
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) acc[m][b] = mfma_h3(af[m], o[b][0], o[b][1], acc[m][b]);
+        };
+        // weight fragments in a ring PSD K tiles deep (the tail reloads the last tile: straight-line steps)
+        u32x4 wr[PSD][TM][NPAC];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          if constexpr (PRE_A) {
+#pragma unroll
+            for (int p3 = 0; p3 < NPAC; ++p3) wr[0][m][p3] = pa0[m][p3];
+          } else {
+            ld3(m, 0, wr[0][m]);
+          }
+        }
+#pragma unroll
+        for (int d = 1; d + 1 < PSD; ++d)
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ld3(m, min(d, nkt - 1), wr[d][m]);
+        for (int kt = 0; kt < nkt; kt += PSD) {
+#pragma unroll
+          for (int d = 0; d < PSD; ++d) {
+#pragma unroll
+            for (int m = 0; m < TM; ++m) ld3(m, min(kt + d + PSD - 1, nkt - 1), wr[(d + PSD - 1) % PSD][m]);
+            if (kt + d < nkt) tileP(kt + d, wr[d]);
+          }
+        }
       } else {
-        gath(kt, xn);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
+        gather_path();
       }
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[m][b] = mma<NPAC>(af[m], bq[b], acc[m][b]);
-      if constexpr (PRE_A) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) splitb<NPAC>(xn[b], sA, bq[b]);
-      }
-    };
-    u32x4 a0[TM][NPAC], a1[TM][NPAC];
-#pragma unroll
-    for (int m = 0; m < TM; ++m) {
-      if constexpr (PRE_A) {
-#pragma unroll
-        for (int p3 = 0; p3 < NPAC; ++p3) a0[m][p3] = pa0[m][p3];
-      } else {
-        ld3(m, 0, a0[m]);
-      }
-    }
-    for (int kt = 0; kt < nkt; kt += 2) {
-      const bool has1 = kt + 1 < nkt;
-      if (has1) {
-#pragma unroll
-        for (int m = 0; m < TM; ++m) ld3(m, kt + 1, a1[m]);
-      }
-      tileA(kt, a0);
-      if (kt + 2 < nkt) {
-#pragma unroll
-        for (int m = 0; m < TM; ++m) ld3(m, kt + 2, a0[m]);
-      }
-      if (has1) tileA(kt + 1, a1);
+    } else {
+      gather_path();
     }
     if constexpr (H3AC) {
 #pragma unroll
@@ -483,7 +590,8 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) dv[r] = swish_fast_d(z, sp1);
           }
           if constexpr (H3) cm[b] = fmaxf(cm[b], fabsf(v));
-          t[o * F_BN + b * 32 + li] = v;
+          if (psb) acc[m][b][r] = v;                  // (pre-split: put below, at the column scales)
+          else t[o * F_BN + b * 32 + li] = v;
         }
         if constexpr (MODE == MODE_SAVE || MODE == MODE_EVALSAVE) store_d(a.d1, m, b, dv);
       }
@@ -500,7 +608,6 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
   STAMP(3);
 
   // ---------------------------------------------------------------- phase B: K = HID (from LDS)
-  zero_acc();
   int hexp[NB];                                      // H3: unscale exponent per pixel column
   if constexpr (H3) {
     constexpr int nkt = HID / 16;
@@ -516,6 +623,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       hs[b] = __builtin_amdgcn_ldexpf(1.f, sc);
       hexp[b] = -(sc + sw);
     }
+    if (psb) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) put_planes(tpl, rbw + m, b, acc[m][b], hs[b]);
+      __syncthreads();
+    }
+    zero_acc();
     auto ld2 = [&](int m, int kt, u32x4 (&o)[2]) {
       const u32x4* q = A2h + ((long)((rbw + m) * nkt + kt) * 2) * 64 + lane;
       o[0] = q[0];
@@ -538,6 +653,36 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[m][b] = mfma_h3(af[m], o.h[b], o.l[b], acc[m][b]);
     };
+    if (psb) {
+      // B operand from the planes; the weight fragments in a ring PSD K tiles deep (32 registers of
+      // accumulators leave the room)
+      u32x4 wr[PSD][TM][2], hb[NB], lb[NB];
+#pragma unroll
+      for (int d = 0; d + 1 < PSD; ++d)
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ld2(m, d, wr[d][m]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        hb[b] = tpl[(b * 2) * 64 + lane];
+        lb[b] = tpl[(b * 2 + 1) * 64 + lane];
+      }
+      static_assert(nkt % PSD == 0, "phase-B K tiles must be a multiple of the ring depth");
+      for (int kt = 0; kt < nkt; kt += PSD) {
+#pragma unroll
+        for (int d = 0; d < PSD; ++d) {
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ld2(m, min(kt + d + PSD - 1, nkt - 1), wr[(d + PSD - 1) % PSD][m]);
+          const int kn = min(kt + d + 1, nkt - 1);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+#pragma unroll
+            for (int m = 0; m < TM; ++m) acc[m][b] = mfma_h3(wr[d][m], hb[b], lb[b], acc[m][b]);
+            hb[b] = tpl[((kn * NB + b) * 2) * 64 + lane];
+            lb[b] = tpl[((kn * NB + b) * 2 + 1) * 64 + lane];
+          }
+        }
+      }
+    } else {
     constexpr int D = 2;
     constexpr bool BPIPE = PB_BPIPE && F_LDS_FLOATS != LDS_HALF;
     u32x4 ab[D][TM][2];
@@ -570,6 +715,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         }
       }
     }
+    }   // (per-wave split)
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -577,6 +723,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[m][b][r] = __builtin_amdgcn_ldexpf(acc[m][b][r], hexp[b]);
   } else if constexpr (SPL) {
+    zero_acc();
     constexpr int nkt = HID / 16;
     const u32x4* A2s = reinterpret_cast<const u32x4*>(a.A2s);
     auto ld3 = [&](int m, int kt, u32x4 (&o)[3]) {
@@ -664,6 +811,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
     __builtin_amdgcn_s_setprio(0);
 #endif
   } else {
+    zero_acc();
     constexpr int nkt = HID / 16;
     auto tileB = [&](int kt, const float (&af)[TM][8]) {
       const float* tb = t + (kt * 16 + lh * 8) * F_BN + li;
@@ -741,13 +889,15 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       if (s_ == 12345.678f) pr.tbuf[0] = 0;
       WSTAMP(16);
     }
-    __syncthreads();
+    if (!psc) {           // (pre-split: nothing is written into the operand buffer before the next barrier)
+      __syncthreads();
 #pragma unroll
-    for (int m = 0; m < TM; ++m)
+      for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
+          for (int r = 0; r < 16; ++r) t[row_of(m, r) * F_BN + b * 32 + li] = acc[m][b][r];
+    }
     if constexpr (H3AC) {
       // phase C's per-column scales (cmax is free again: every wave read it before phase B, i.e. before the
       // barrier above)
@@ -772,6 +922,21 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       const int sc = h3_scale_exp(m_);
       S = __builtin_amdgcn_ldexpf(1.f, sc);
       e = -(sc + ldc(a.Ah_exp + 2));
+    };
+    if (psc) {            // phase C's operand planes at the column scales (every wave is past phase B's reads)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float S;
+        int e_;
+        colscale(b, S, e_);
+#pragma unroll
+        for (int m = 0; m < TM; ++m) put_planes(tpl, rbw + m, b, acc[m][b], S);
+      }
+      __syncthreads();
+    }
+    auto bplane = [&](int b, int kt, u32x4 (&o)[NPAC]) {
+      o[0] = tpl[((kt * NB + b) * 2) * 64 + lane];
+      o[1] = tpl[((kt * NB + b) * 2 + 1) * 64 + lane];
     };
 
     // -------------------------------------------------------------- phase C: taps, K = HID
@@ -821,9 +986,12 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
           };
           // B operand one K tile ahead: its LDS reads and split overlap this tile's MFMA chain
           u32x4 bq[NPAC];
-          if constexpr (PRE_A) bsplit(k_lo, bq);
+          if (PRE_A && !psc) bsplit(k_lo, bq);
           auto step = [&](int kt, const u32x4 (&af)[NPAC]) {
-            if constexpr (PRE_A) {
+            if (psc) {
+              bplane(b, kt, bq);
+              cacc[0] = mma<NPAC>(af, bq, cacc[0]);
+            } else if constexpr (PRE_A) {
               float xn[8];
               bread(b, min(kt + 1, k_hi - 1), xn);
               cacc[0] = mma<NPAC>(af, bq, cacc[0]);
@@ -890,8 +1058,15 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             rbj[g] = vj[g] ? job / NB : job0 / NB;
           }
           u32x4 bq[NPAC];
-          if constexpr (PRE_A) bsplit(0, bq);
+          if (PRE_A && !psc) bsplit(0, bq);
           auto step = [&](int kt, const u32x4 (&af)[G][NPAC]) {
+            if (psc) {
+              bplane(b, kt, bq);
+#pragma unroll
+              for (int g = 0; g < G; ++g)
+                if (vj[g]) cacc[G * jp + g] = mma<NPAC>(af[g], bq, cacc[G * jp + g]);
+              return;
+            }
             float xn[8];
             if constexpr (PRE_A) bread(b, min(kt + 1, nkt - 1), xn);
             else bsplit(kt, bq);
@@ -1102,6 +1277,13 @@ static void timing_collect(const char* key, long nwg, hipStream_t s) {
   }
 }
 
+// XCD_PAIRS=1 builds place the two nets of a pair launch on different XCDs (Net313Pair::xcd).  Measured and not kept as
+// the default (round 6): the per-launch kernel times did not move (k128 VJP 15.74 vs 15.76 ms per step,
+// s2 VJP 3.21 vs 3.16), so each XCD's L2 already serves both nets' weight planes
+#ifndef XCD_PAIRS
+#define XCD_PAIRS 0
+#endif
+
 int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hipStream_t s, int layout_nets) {
   if (layout_nets <= 0) layout_nets = nnets;
   const Net313Args& a0 = args[0];
@@ -1134,8 +1316,9 @@ int launch_net313_multi(const Net313Args* args, int nnets, int hid, int mode, hi
   for (int i = 0; i < 2; ++i) pr.a[i].seg = a0.W < tbn ? a0.W : tbn;
   pr.nb0 = a0.B * (P / tbn);
   pr.max_ksplit = 8;
-  pr.dbg = a0.exact_scale ? 16 : 0;        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile
+  pr.dbg = (a0.exact_scale ? 16 : 0) | (a0.presplit ? 0 : 32);        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile
   pr.reverse = a0.tile_order;
+  pr.xcd = XCD_PAIRS && nnets == 2 && (pr.nb0 * 2) % 8 == 0;
   pr.tbuf = nullptr;
   if (INFLOW_PHASE_STAMPS) pr.tbuf = timing_buf(pr.nb0 * nnets);   // tools/build_alt_k128.py "stamps" builds only
   const unsigned nb = (unsigned)(pr.nb0 * nnets);

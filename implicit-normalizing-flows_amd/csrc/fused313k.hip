@@ -50,6 +50,9 @@ constexpr int KB_HID = 512;
 constexpr int KB_LDS = 40960;       // floats (160 KiB)
 constexpr int KB_CHUNK = 32768;     // floats: 16 K tiles x 4 column blocks x 2 planes x 64 lanes x 16 B
 constexpr int KB_TSLOTS = 32;
+#ifndef K128_PSA
+#define K128_PSA 1                  // phase A's im2col planes split once per workgroup (0: per wave, A/B builds)
+#endif
 
 // the two (h, l) planes of fragment tile `tile` (fragment-major, launch_split2h order)
 __device__ __forceinline__ void ldw2(const u32x4* base, long tile, int lane, u32x4 (&o)[2]) {
@@ -94,9 +97,9 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   // fragment order (the order this kernel's VJP reads them in); MODE_SAVE stops after phase B
   constexpr bool SAVE = MODE == MODE_SAVE || MODE == MODE_EVALSAVE;
   const int bx = pr.reverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
-  const int sel = bx >= pr.nb0 ? 1 : 0;
+  int sel;
+  const int bid = pair_tile(pr, bx, sel);
   const Net313Args& a = pr.a[sel];
-  const int bid = bx - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[KB_LDS];
 #define KSTAMP(i_)                                                                             \
   do {                                                                                         \
@@ -314,6 +317,33 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     sA = __builtin_amdgcn_ldexpf(1.f, sc);
     eA = -(sc + ldc(a.Ah_exp));
   }
+  // Phase A's im2col operand pre-split (INF_OPT_FUSED_PRESPLIT; the 3-channel scales, where its planes fit beside the
+  // halo): the B fragments of phase A are the same for both chunks and every wave (only the weight rows differ), so
+  // they are gathered from the halo and split into their fp16 (h, l) planes once per workgroup, one (K tile, column
+  // block, lane) slot per thread, instead of 8 gathered ds_read_b32 and the split per wave, K tile, column block and
+  // chunk.  Same scale, same rounding: bitwise the same results.
+  constexpr int SEGc = WT ? kb_seg(WT) : 1, ROWSc = KB_BN / SEGc;
+  constexpr int VHZc = CT * (ROWSc + 2) * (SEGc + 2) + ROWSc * (SEGc + 2);
+  constexpr int VH_OFF = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + 4 + (9 * CT + 15) / 16 * 16;
+  constexpr bool PSA = K128_PSA && CT > 0 && WT > 0 && VH_OFF + ((VHZc + 3) & ~3) + NKT1 * KB_NB * 512 <= KB_LDS;
+  constexpr bool psa = PSA;           // (compile-time: a runtime switch costs the VJP 17 more spilled VGPRs)
+  u32x4* const pa = reinterpret_cast<u32x4*>(vh + ((vhz + 3) & ~3));
+  if constexpr (psa) {
+    for (int s_ = tid; s_ < NKT1 * KB_NB * 64; s_ += KB_NT) {
+      const int kt = s_ / (KB_NB * 64), rem = s_ - kt * (KB_NB * 64), b = rem >> 6, ln = rem & 63;
+      const int n = b * 32 + (ln & 31), py = n / seg;
+      const int px_ = py * CW + (n - py * seg);
+      const int* kp = koff + kt * 16 + (ln >> 5) * 8;
+      float x[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) x[kk] = vh[kp[kk] + px_];
+      u32x4 h, l;
+      split2h(x, sA, h, l);
+      pa[((kt * KB_NB + b) * 2) * 64 + ln] = h;
+      pa[((kt * KB_NB + b) * 2 + 1) * 64 + ln] = l;
+    }
+    __syncthreads();
+  }
   const u32x4* A1h = reinterpret_cast<const u32x4*>(a.A1h);
   const u32x4* A2h = reinterpret_cast<const u32x4*>(a.A2h);
   const u32x4* A3p = reinterpret_cast<const u32x4*>(a.A3p);
@@ -369,6 +399,15 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       constexpr bool PRE = c == 0 ? PRE_A0 : PRE_A1;
       if (!PRE) ldw2(A1h, (long)rbA * nkt1, lane, w0);
       auto stepA = [&](int kt, const u32x4 (&af)[2]) {
+        if constexpr (psa) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const u32x4 h = pa[((kt * KB_NB + b0 + g) * 2) * 64 + lane];
+            const u32x4 l = pa[((kt * KB_NB + b0 + g) * 2 + 1) * 64 + lane];
+            ac[g] = mfma_h3(af, h, l, ac[g]);
+          }
+          return;
+        }
         const int* kp = koff + kt * 16 + lh * 8;
         const int4 k0 = *reinterpret_cast<const int4*>(kp);
         const int4 k1 = *reinterpret_cast<const int4*>(kp + 4);

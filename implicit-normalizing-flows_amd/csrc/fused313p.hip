@@ -67,9 +67,9 @@ int net313p_fits(int hid, int C, int H, int W) {
 template <int CT, int WT>
 __global__ __launch_bounds__(PB_NT) __attribute__((amdgpu_waves_per_eu(2))) void net313p_kernel(Net313Pair pr) {
   const int bx = pr.reverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
-  const int sel = bx >= pr.nb0 ? 1 : 0;
+  int sel;
+  const int bid = pair_tile(pr, bx, sel);
   const Net313Args& a = pr.a[sel];
-  const int bid = bx - (sel ? pr.nb0 : 0);
   __shared__ __attribute__((aligned(16))) float smem[PB_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, lh = lane >> 5;

@@ -56,6 +56,8 @@ struct OutArgs {
   const float* pre_beta;  // OM_VJP: multiply by swish'(in1) (preact input derivative)
   double* partial;        // (B, nchunk) per-sample partial sums (OM_RESID: g^2, OM_VJP: v.eps)
   int nchunk;
+  int sample_sums;        // OM_RESID, conv nets: one block per sample writes the sample's total to partial[b] (the chunk
+                          // partials summed in chunk order, as launch_reduce_partials does: the same bits)
   // host side (not read by the kernels): an event for the launch itself to complete (hipExtLaunchKernel's stop event:
   // no marker packet after it), and the flag the launcher sets when it bound it (fc readbacks, engine.hip enqueue_sumsq)
   hipEvent_t stop_ev = nullptr;
@@ -141,8 +143,11 @@ int launch_logdet_pairs(int mode, const float* tang, const float* eps, const flo
                         const float* coeff_host, int n_terms, int d, int batch, float* A, float* bv, float* xr,
                         float* value, float* a_scr, hipStream_t s);
 int launch_sum_pairs(const float* gs, int T, int d, int batch, float* gx, hipStream_t s);
+// sample_sums: one block per sample, partial[b] = the sample's total (conv_out's OutArgs::sample_sums); stop_ev: the
+// launch completes it (hipExtLaunchKernel, not while profiling), *stop_bound set
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
-                       int batch, int per, int nchunk, hipStream_t s);
+                       int batch, int per, int nchunk, hipStream_t s, int sample_sums = 0, hipEvent_t stop_ev = nullptr,
+                       bool* stop_bound = nullptr);
 // fc layout (d, B): f0 holds d values
 int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                           int batch, int d, hipStream_t s);
@@ -206,6 +211,7 @@ struct Net313Args {
   int k128;               // tile policy of the net (INF_OPT_FUSED_K128): 0 64-px only, 1 128-px where the grid
                           //   covers every CU, 2 128-px wherever it fits; a pair launch follows args[0]
   int tile_order;         // 1: the 128-pixel kernel walks the tiles backwards (series terms alternate; args[0])
+  int presplit;           // INF_OPT_FUSED_PRESPLIT: the wide 32-pixel kernel's B operands split once in LDS (args[0])
   int exact_scale;        // INF_OPT_K128_EXACT_SCALE: chunk 1's exact-scale path on every tile (args[0]; tests)
 };
 struct Net313Pair {
@@ -213,9 +219,21 @@ struct Net313Pair {
   int nb0;                // workgroups of net 0; blocks >= nb0 run net 1
   int max_ksplit;         // cap on phase C's K split (8)
   unsigned long long* tbuf;   // INFLOW_PHASE_STAMPS builds only: per-workgroup s_memtime stamps at phase boundaries
-  int dbg;                // bit 16: the 128-pixel kernel's chunk-1 exact-scale path on every tile (results unchanged)
+  int dbg;                // bit 16: the 128-pixel kernel's chunk-1 exact-scale path on every tile (results unchanged);
+                          // bit 32: the wide 32-pixel kernel splits its B operands per consuming wave (no pre-split)
   int reverse;            // 128-pixel kernel: workgroup i runs tile nb - 1 - i (alternating series terms)
+  int xcd;                // two nets, 8 | grid: blocks b with (b & 7) < 4 run net 0, the others net 1 (blocks b and
+                          // b + 8 share an XCD, MI355X_MICROARCH.md), so each XCD's L2 holds one net's weight planes
 };
+// (net, tile) of a pair launch's workgroup `bx` (after any reversal); speed-only placement, results do not depend on it
+__device__ __forceinline__ int pair_tile(const Net313Pair& pr, int bx, int& sel) {
+  if (pr.xcd) {
+    sel = (bx & 7) >> 2;
+    return (bx >> 3) * 4 + (bx & 3);
+  }
+  sel = bx >= pr.nb0 ? 1 : 0;
+  return bx - (sel ? pr.nb0 : 0);
+}
 int net313_supported(int hid, int C, int H, int W);
 // 128-pixel K-chunked variant (fused313k.hip, INF_MFMA_F16X3 only): MODE_VJP and MODE_EVAL
 int net313k_fits(int hid, int C, int H, int W);

@@ -86,10 +86,79 @@ __global__ __launch_bounds__(OUT_CH) void conv_out_kernel(OutArgs a) {
   }
 }
 
+// OM_RESID with the per-sample total (OutArgs::sample_sums, at most SS_MAXCH chunks per sample): one block per sample, its
+// threads each taking one element of every chunk (all loads of the sample issued before the sums), the chunk sums formed
+// as conv_out_kernel's blocks form them and added in chunk order from 0.0, as reduce_partials_kernel does -- the same
+// bits, without the reduction launch; partial[b] is the sample's total (the pinned readback slot in broyden_core).
+constexpr int SS_MAXCH = 4;
+template <int KS, int NCH>
+__global__ __launch_bounds__(OUT_CH) void conv_out_resid_sample_kernel(OutArgs a) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const int P = a.H * a.W, per = a.C * P;
+  const long ybase = (long)b * a.y_sample, ebase = (long)b * per;
+  double acc[NCH];
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    acc[cc] = 0.0;
+    const int i = cc * OUT_CH + threadIdx.x;
+    if (i >= per) continue;
+    const int c = i / P, p = i - c * P;
+    float sv;
+    if constexpr (KS == 1) {
+      sv = a.Y[ybase + (long)c * P + p];
+    } else {
+      const int y = p / a.W, x = p - y * a.W;
+      const float* yc = a.Y + ybase + (long)c * 9 * P;
+      sv = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) sv += yc[(long)t * P + yy * a.W + xx];
+      }
+    }
+    const long ei = ebase + i;
+    const float v = sv + a.bias[c];
+    const float gx = (a.in0[ei] - v) - a.in1[ei];
+    a.out0[ei] = gx;
+    if (a.in2) a.out1[ei] = gx - a.in2[ei];
+    if (a.out2) a.out2[ei] = v;
+    acc[cc] += (double)gx * (double)gx;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    const double t = block_sum(acc[cc], red);
+    tot += t;
+  }
+  if (threadIdx.x == 0) a.partial[b] = tot;
+}
+
 int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
   const int per = a.C * a.H * a.W;
   dim3 grid(out_nchunk(per), batch);
   const bool prof = prof_enabled();
+  if (a.sample_sums) {
+    const int nch = out_nchunk(per);
+    if (a.mode != OM_RESID || nch > SS_MAXCH || !a.partial) return INF_ERR_INVALID;
+    const void* fn = nullptr;
+#define SS_K(KS_, N_)                                                                           \
+    if (a.ks == KS_ && nch == N_) fn = reinterpret_cast<const void*>(&conv_out_resid_sample_kernel<KS_, N_>);
+    SS_K(3, 1) SS_K(3, 2) SS_K(3, 3) SS_K(3, 4) SS_K(1, 1) SS_K(1, 2) SS_K(1, 3) SS_K(1, 4)
+#undef SS_K
+    if (!fn) return INF_ERR_INVALID;
+    OutArgs ka = a;
+    void* args[] = {&ka};
+    if (a.stop_ev && !prof) {          // the launch completes the readback slot's event (no marker packet)
+      INF_HIP(hipExtLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s, nullptr, a.stop_ev, 0));
+      if (a.stop_bound) *a.stop_bound = true;
+      return INF_OK;
+    }
+    if (prof) prof_begin_launch(s);
+    INF_HIP(hipLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s));
+    if (prof) prof_end_launch(s, 900 + a.mode * 10 + a.ks, 0.0, 4.0 * (double)batch * per * (a.ks == 3 ? 9 : 1) + 12.0 * (double)batch * per);
+    return INF_OK;
+  }
   if (prof) prof_begin_launch(s);
   if (a.ks == 1)
     hipLaunchKernelGGL(conv_out_kernel<1>, grid, dim3(OUT_CH), 0, s, a);
@@ -105,7 +174,8 @@ int launch_conv_out(const OutArgs& a, int batch, hipStream_t s) {
 }
 
 // First Broyden residual from the cached f(0) (conv nets): v = f0[i] for every sample,
-// g = (x_embed - v) - z exactly as conv_out's OM_RESID, fcur = v, per-sample partial sums of g^2.
+// g = (x_embed - v) - z exactly as conv_out's OM_RESID, fcur = v, per-sample partial sums of g^2 (NCH > 0: one block per
+// sample, the sample's total in partial[b], summed as conv_out_resid_sample_kernel does).
 __global__ __launch_bounds__(OUT_CH) void resid_bcast_kernel(const float* f0, const float* xemb, const float* z, float* g,
                                                           float* fcur, double* partial, int per, int nchunk) {
   __shared__ double red[16];
@@ -123,8 +193,54 @@ __global__ __launch_bounds__(OUT_CH) void resid_bcast_kernel(const float* f0, co
   const double t = block_sum(acc, red);
   if (threadIdx.x == 0) partial[(long)b * nchunk + chunk] = t;
 }
+template <int NCH>
+__global__ __launch_bounds__(OUT_CH) void resid_bcast_sample_kernel(const float* f0, const float* xemb, const float* z,
+                                                                 float* g, float* fcur, double* partial, int per) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const long base = (long)b * per;
+  double acc[NCH];
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    acc[cc] = 0.0;
+    const int i = cc * OUT_CH + threadIdx.x;
+    if (i >= per) continue;
+    const float v = f0[i];
+    const float gx = (xemb[base + i] - v) - z[base + i];
+    g[base + i] = gx;
+    fcur[base + i] = v;
+    acc[cc] += (double)gx * (double)gx;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    const double t = block_sum(acc[cc], red);
+    tot += t;
+  }
+  if (threadIdx.x == 0) partial[b] = tot;
+}
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
-                       int batch, int per, int nchunk, hipStream_t s) {
+                       int batch, int per, int nchunk, hipStream_t s, int sample_sums, hipEvent_t stop_ev,
+                       bool* stop_bound) {
+  if (sample_sums) {
+    const int nch = out_nchunk(per);
+    const void* fn = nch == 1 ? reinterpret_cast<const void*>(&resid_bcast_sample_kernel<1>)
+                   : nch == 2 ? reinterpret_cast<const void*>(&resid_bcast_sample_kernel<2>)
+                   : nch == 3 ? reinterpret_cast<const void*>(&resid_bcast_sample_kernel<3>)
+                   : nch == 4 ? reinterpret_cast<const void*>(&resid_bcast_sample_kernel<4>) : nullptr;
+    if (!fn) return INF_ERR_INVALID;
+    void* args[] = {&f0, &xemb, &z, &g, &fcur, &partial, &per};
+    const bool prof = prof_enabled();
+    if (stop_ev && !prof) {
+      INF_HIP(hipExtLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s, nullptr, stop_ev, 0));
+      if (stop_bound) *stop_bound = true;
+      return INF_OK;
+    }
+    if (prof) prof_begin_launch(s);
+    INF_HIP(hipLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s));
+    if (prof) prof_end_launch(s, 700, 0.0, 16.0 * batch * per + 4.0 * per);
+    return INF_OK;
+  }
   INF_PROF_LAUNCH(s, 700, 16.0 * batch * per + 4.0 * per, resid_bcast_kernel, dim3(out_nchunk(per), batch),
                   dim3(OUT_CH), 0, s, f0, xemb, z, g, fcur, partial, per, nchunk);
   return INF_OK;
@@ -703,6 +819,144 @@ __global__ __launch_bounds__(256) void broyden_p4(BroydenArgs a, int nchunk, int
   }
 }
 
+// The whole update in one launch for d <= BR_FUSED_CH chunks (CIFAR-10: d = 3072, 3 chunks): one workgroup per sample;
+// its thread group g (256 threads) does for chunk g exactly what one block of broyden_p1..p4 does (same elements per
+// thread, same accumulation order, the same wave sums added in wave order for the chunk's block sum, the chunk sums in
+// chunk order), so the results are bitwise those of the four launches.  The chunk partials stay in LDS, and U_m / VT_m
+// and this thread's d-vector elements stay in registers between the stages (the three launches in between, each
+// waiting for CUs beside the other branch's series in the overlapped schedule, are gone).
+constexpr int BR_FUSED_CH = 4;
+__global__ __launch_bounds__(256 * BR_FUSED_CH) void broyden_fused_kernel(BroydenArgs a, int nchunk) {
+  constexpr int PER = BR_CH / 256;                   // elements per thread and chunk (as in the chunked kernels)
+  __shared__ double ws[4 * BR_FUSED_CH][2 * BR_TMAX];
+  __shared__ float coef[2 * BR_TMAX];
+  __shared__ float denf;
+  const int b = blockIdx.x;
+  const int g = threadIdx.x >> 8, tg = threadIdx.x & 255, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lo = g * BR_CH, hi = min(a.d, lo + BR_CH);
+  long e[PER];
+  bool ok[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = lo + tg + 256 * k;
+    ok[k] = i < hi;
+    e[k] = BR_IDX(b, ok[k] ? i : lo);
+  }
+  if (a.active && !a.active[b]) {                    // (broyden_p4's stopped sample; p1..p3 skip it)
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (ok[k]) {
+        a.xnew[e[k]] = a.x[e[k]];
+        a.dxnew[e[k]] = 0.f;
+        a.upd[e[k]] = 0.f;
+      }
+    return;
+  }
+  float dx[PER], dg[PER], gx[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    dx[k] = ok[k] ? a.dx[e[k]] : 0.f;
+    dg[k] = ok[k] ? a.dg[e[k]] : 0.f;
+    gx[k] = ok[k] ? a.gx[e[k]] : 0.f;
+  }
+  // chunk sum of column jj from the per-wave sums: the chunk's 4 waves in order, then the chunks in order
+  auto csum = [&](int jj) {
+    double s = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+      double r = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r += ws[4 * c + i][jj];
+      s += r;
+    }
+    return s;
+  };
+  // p1: a_j = dx . U_j, c_j = VT_j . dg (j < m)
+  for (int j = 0; j < a.m; ++j) {
+    const float* U = a.U + (long)j * a.cs;
+    const float* V = a.VT + (long)j * a.cs;
+    double sa = 0.0, sc = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (ok[k]) {
+        sa += (double)dx[k] * U[e[k]];
+        sc += (double)V[e[k]] * dg[k];
+      }
+    sa = wave_sum(sa);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+      ws[w][j] = sa;
+      ws[w][BR_TMAX + j] = sc;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * a.m; j += blockDim.x) coef[j] = (float)csum(j < a.m ? j : BR_TMAX + (j - a.m));
+  __syncthreads();
+  // p2: VT_m, U_m and the denominator
+  float vt[PER], um[PER];
+  double den = 0.0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!ok[k]) continue;
+    float v_ = -dx[k], t = -dg[k];
+    for (int j = 0; j < a.m; ++j) {
+      v_ += coef[j] * a.VT[(long)j * a.cs + e[k]];
+      t += coef[a.m + j] * a.U[(long)j * a.cs + e[k]];
+    }
+    vt[k] = v_;
+    um[k] = dx[k] - t;
+    den += (double)v_ * dg[k];
+  }
+  den = wave_sum(den);
+  if (lane == 0) ws[w][0] = den;
+  __syncthreads();
+  if (threadIdx.x == 0) denf = (float)csum(0);
+  __syncthreads();
+  // p3: scale U_m, scrub NaN, store U_m / VT_m; e_j = VT_j . gx (j < ncols; VT_m from registers)
+  float* Um = a.U + (long)a.m * a.cs;
+  float* Vm = a.VT + (long)a.m * a.cs;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!ok[k]) continue;
+    float v_ = vt[k];
+    float u = um[k] / denf;
+    if (v_ != v_) v_ = 0.f;
+    if (u != u) u = 0.f;
+    vt[k] = v_;
+    um[k] = u;
+    Vm[e[k]] = v_;
+    Um[e[k]] = u;
+  }
+  for (int j = 0; j < a.ncols; ++j) {
+    const float* V = a.VT + (long)j * a.cs;
+    double se = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (ok[k]) se += (double)(j == a.m ? vt[k] : V[e[k]]) * gx[k];
+    se = wave_sum(se);
+    if (lane == 0) ws[w][j] = se;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < a.ncols; j += blockDim.x) coef[j] = (float)csum(j);
+  __syncthreads();
+  // p4: update = -(-gx + sum_j e_j U_j), x_new, dx_new
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (!ok[k]) continue;
+    float t = -gx[k];
+    for (int j = 0; j < a.ncols; ++j) t += coef[j] * (j == a.m ? um[k] : a.U[(long)j * a.cs + e[k]]);
+    const float up = -t;
+    a.upd[e[k]] = up;
+    const float x0 = a.x[e[k]];
+    const float xe = x0 + up;
+    a.xnew[e[k]] = xe;
+    a.dxnew[e[k]] = xe - x0;
+  }
+}
+
+#ifndef BR_FUSED
+#define BR_FUSED 1      // 0: the chunked four-launch update for every d (A/B builds)
+#endif
+
 int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
   if (a.T > BR_TMAX || a.m >= a.T || a.ncols > a.T) return INF_ERR_INVALID;
   // algorithmic bytes (fp32, D = batch x d): each kernel's distinct reads and writes of the d-vectors and U / VT columns
@@ -718,6 +972,12 @@ int launch_broyden_update(const BroydenArgs& a, hipStream_t s) {
     return INF_OK;
   }
   const int nchunk = (a.d + BR_CH - 1) / BR_CH;
+  if (BR_FUSED && nchunk <= BR_FUSED_CH) {
+    // dx, dg, gx, x; U_j, VT_j (j < m); writes U_m, VT_m, update, x_new, dx_new
+    INF_PROF_LAUNCH(s, 716, D4 * (9.0 + 2.0 * a.m), broyden_fused_kernel, dim3(a.batch), dim3(256 * nchunk), 0, s, a,
+                    nchunk);
+    return INF_OK;
+  }
   dim3 grid(nchunk, a.batch);
   double* part2 = a.part + (long)a.batch * nchunk * 2 * a.T;
   double* part3 = part2 + (long)a.batch * nchunk;

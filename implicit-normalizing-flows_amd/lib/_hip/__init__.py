@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('INFLOW_LIB') or LIB_PATH   # development knob: an alt
 INF_LAYER_CONV, INF_LAYER_LINEAR, INF_ACT_SWISH, INF_ACT_SIN = 1, 2, 3, 4
 INF_ERR_UNSUPPORTED = 4       # InfStatus (include/inflow.h)
 INF_OPT_FUSED_K128, INF_OPT_EVAL_OVERLAP, INF_OPT_CONVERGENCE, INF_OPT_K128_EXACT_SCALE = 1, 2, 3, 4   # InfNetOption
-INF_OPT_FC_BLOCK, INF_OPT_FC_SERIES, INF_OPT_LINE_SEARCH = 5, 6, 7
+INF_OPT_FC_BLOCK, INF_OPT_FC_SERIES, INF_OPT_LINE_SEARCH, INF_OPT_FUSED_PRESPLIT = 5, 6, 7, 8
 INF_CONV_GLOBAL, INF_CONV_PER_SAMPLE = 0, 1                                # InfConvergence
 CONVERGENCE = {'global': INF_CONV_GLOBAL, 'per_sample': INF_CONV_PER_SAMPLE}
 
@@ -463,7 +463,7 @@ PHASE_TAGS = {
     700: 'resid_bcast_kernel', 701: 'resid_bcast_fc_kernel', 702: 'broyden_start_fc_kernel', 703: 'axpy_step_kernel',
     704: 'neg_kernel', 705: 'reduce_partials_kernel', 706: 'recomp_kernel', 707: 'line_step_kernel',
     710: 'broyden_p1', 711: 'broyden_p2', 712: 'broyden_p3', 713: 'broyden_p4', 714: 'br_sum_chunks',
-    715: 'broyden_small_d_kernel',
+    715: 'broyden_small_d_kernel', 716: 'broyden_fused_kernel',
     720: 'series_combine_kernel', 721: 'rademacher_kernel',
 }
 

@@ -165,6 +165,10 @@ int inf_net_get_mfma(const InfNet* net);
  *                         every trial point's norm read back; stats.tnstep counts the accepted searches' iterations
  *                         (:156).  The global rule only (INF_ERR_UNSUPPORTED with INF_CONV_PER_SAMPLE); the fc block
  *                         kernel is not used with it.
+ *   INF_OPT_FUSED_PRESPLIT  1 (default) / 0: the 32-pixel wide-net VJP / forward kernel (net313_kernel_w: CIFAR-10's
+ *                         8x8 scale) splits each phase's B operand into its fp16 (h, l) planes once, in LDS, where it is
+ *                         produced (phase A's im2col after the halo staging, phases B and C in the epilogues before
+ *                         them); 0 splits it per consuming wave, as before round 6.  Bitwise the same results.
  * Unknown values of INFLOW_FUSED_K128 (0-3), INFLOW_FC_BLOCK (0/1/2), INFLOW_EVAL_OVERLAP / INFLOW_FC_SERIES (0/1) and INFLOW_CONVERGENCE (global/per_sample)
  * make inf_net_create fail with INF_ERR_INVALID.
  * FUSED_K128, EVAL_OVERLAP and K128_EXACT_SCALE are performance / test knobs without a reference counterpart (the reference
@@ -172,7 +176,7 @@ int inf_net_get_mfma(const InfNet* net);
  * agree to fp32 roundoff across their values. */
 typedef enum InfNetOption {
   INF_OPT_FUSED_K128 = 1, INF_OPT_EVAL_OVERLAP = 2, INF_OPT_CONVERGENCE = 3, INF_OPT_K128_EXACT_SCALE = 4,
-  INF_OPT_FC_BLOCK = 5, INF_OPT_FC_SERIES = 6, INF_OPT_LINE_SEARCH = 7
+  INF_OPT_FC_BLOCK = 5, INF_OPT_FC_SERIES = 6, INF_OPT_LINE_SEARCH = 7, INF_OPT_FUSED_PRESPLIT = 8
 } InfNetOption;
 typedef enum InfConvergence { INF_CONV_GLOBAL = 0, INF_CONV_PER_SAMPLE = 1 } InfConvergence;
 int inf_net_set_option(InfNet* net, int option, int value);

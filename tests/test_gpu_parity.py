@@ -487,6 +487,55 @@ def test_update_lipschitz_batch_matches_per_layer():
     assert n > 0
 
 
+@pytest.mark.parametrize('C,H,B', [(48, 8, 64), (48, 8, 3), (48, 64, 2), (192, 32, 2)])
+def test_wide_presplit_bitwise(C, H, B):
+    """INF_OPT_FUSED_PRESPLIT: the 32-pixel wide kernel (net313_kernel_w; CIFAR-10's 8x8 scale at the bench batch, the
+    CelebA-HQ 256 64x64 / 32x32 scales) with every phase's B operand split once into fp16 planes in LDS, against the
+    same kernel splitting it per consuming wave: the same scales and roundings, so forward, VJP and the chained series
+    must agree bit for bit (at C = 192 phase A's planes do not fit and only phases B and C take them).  Workspace and
+    LDS NaN-poisoned before every call."""
+    from lib.layers.base import InducedNormConv2d, Swish
+    torch.manual_seed(3)
+    conv = lambda a, b, k: InducedNormConv2d(a, b, k, 1, k // 2, coeff=0.9, atol=1e-3, rtol=1e-3)
+    seq = torch.nn.Sequential(Swish(), conv(C, 512, 3), Swish(), conv(512, 512, 1), Swish(), conv(512, C, 3)).to(DEV)
+    with torch.no_grad():
+        seq(torch.zeros(1, C, H, H, device=DEV))
+        for m in seq:
+            if isinstance(m, Swish):
+                m.beta.fill_(0.4)
+    x = (torch.randn(B, C, H, H) * 0.5).to(DEV)
+    v = torch.randn(B, C, H, H).to(DEV)
+    net = _hip.NativeNet(_hip.net_entries(seq), (C, H, H), x.device)
+    stream = _hip.stream_of(x)
+    net.refresh_if_needed(stream)
+    ws = torch.empty(net.ws_bytes(B), dtype=torch.uint8, device=DEV)
+    co = np.array([(-1) ** (k + 1) / k for k in range(1, 9)], dtype=np.float32)
+    outs = {}
+    for ps in (1, 0):
+        assert net.lib.inf_net_set_option(net.handle, _hip.INF_OPT_FUSED_PRESPLIT, ps) >= 0
+        assert net.lib.inf_net_get_option(net.handle, _hip.INF_OPT_FUSED_PRESPLIT) == ps
+
+        def poison():
+            ws.fill_(255)
+            _hip.check(net.lib.inf_debug_poison_lds(stream), 'poison_lds')
+        y, g, ld = torch.empty_like(x), torch.empty_like(x), torch.empty(B, device=DEV)
+        poison()
+        _hip.check(net.lib.inf_net_forward(net.handle, _hip.ptr(x), _hip.ptr(y), B, _hip.ptr(ws), ws.numel(), stream),
+                   'fwd')
+        poison()
+        _hip.check(net.lib.inf_net_vjp(net.handle, _hip.ptr(x), _hip.ptr(v), _hip.ptr(g), B, _hip.ptr(ws), ws.numel(),
+                                       stream), 'vjp')
+        poison()
+        _hip.check(net.lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(torch.sign(v)),
+                                             co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 8, _hip.ptr(ld), B,
+                                             _hip.ptr(ws), ws.numel(), stream), 'series')
+        torch.cuda.synchronize()
+        outs[ps] = (y, g, ld)
+    for a, b in zip(outs[1], outs[0]):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b), (a - b).abs().max().item()
+
+
 @pytest.mark.parametrize('C,H,hid,B', [(48, 64, 512, 2), (192, 32, 512, 2), (3, 32, 256, 8), (12, 16, 256, 2)])
 @pytest.mark.parametrize('mfma', [0, 1, 2])
 def test_fused_wide_variant_matches_generic(C, H, hid, B, mfma, monkeypatch):

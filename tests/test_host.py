@@ -46,7 +46,8 @@ def test_no_process_wide_switches():
     assert not hasattr(lib, 'inf_set_fused_k128') and not hasattr(lib, 'inf_set_eval_overlap')
     lib = _hip.load()
     for opt in (_hip.INF_OPT_FUSED_K128, _hip.INF_OPT_EVAL_OVERLAP, _hip.INF_OPT_CONVERGENCE,
-                _hip.INF_OPT_K128_EXACT_SCALE, _hip.INF_OPT_FC_BLOCK, _hip.INF_OPT_FC_SERIES):
+                _hip.INF_OPT_K128_EXACT_SCALE, _hip.INF_OPT_FC_BLOCK, _hip.INF_OPT_FC_SERIES, _hip.INF_OPT_LINE_SEARCH,
+                _hip.INF_OPT_FUSED_PRESPLIT):
         assert lib.inf_net_set_option(None, opt, 0) == -1
         assert lib.inf_net_get_option(None, opt) == -1
 
@@ -67,7 +68,7 @@ def test_kernel_sources_read_no_tuning_environment():
         if f == 'engine.hip':   # the option defaults are parsed from a table of names
             names |= {n for n in re.findall(r'"(INFLOW_[A-Z0-9_]+)"', src)}
     assert names - allowed <= {'INFLOW_FUSED_K128', 'INFLOW_EVAL_OVERLAP', 'INFLOW_CONVERGENCE', 'INFLOW_FC_BLOCK',
-                              'INFLOW_FC_SERIES'}, names
+                              'INFLOW_FC_SERIES', 'INFLOW_FUSED_PRESPLIT'}, names
 
 
 def test_sharded_probes_are_rows_of_the_global_draw():

@@ -14,6 +14,7 @@ import torch  # noqa: E402
 from lib import _hip, synthetic as syn  # noqa: E402
 from lib.configs import build_flow, engine_nets, imblocks  # noqa: E402
 from lib.density import tabular_logpx  # noqa: E402
+import atexit  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument('--arch', default='power')
@@ -21,7 +22,13 @@ ap.add_argument('--batch', type=int, default=1000)
 ap.add_argument('--reps', type=int, default=5)
 ap.add_argument('--modes', default='global,per_sample')
 ap.add_argument('--fcb', default='1,0')
+ap.add_argument('--maps', default='', help='write /proc/self/maps here at exit (maps exit-time crash frames to libraries)')
 a = ap.parse_args()
+if a.maps:
+    def _dump_maps(path=a.maps):
+        with open('/proc/self/maps') as f, open(path, 'w') as o:
+            o.write(f.read())
+    atexit.register(_dump_maps)   # (registered after lib._hip's: runs first)
 arch = syn.POWER if a.arch == 'power' else syn.TOY
 B = a.batch
 m = build_flow(arch, B)
