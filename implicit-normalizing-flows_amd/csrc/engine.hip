@@ -3239,6 +3239,48 @@ size_t inf_grad_workspace_bytes(InfNet* n, int B) {
 
 int inf_debug_poison_lds(void* stream) { return glue_poison_lds((hipStream_t)stream); }
 
+// readback contract check (inflow.h): round r writes base_r + i (i < n) into a pinned coherent slot, once from a kernel
+// whose launch completes the slot's event (the zero-copy Broyden sums) and once through a device buffer and a D2H copy
+// followed by a recorded event (the reduction + copy form); the host waits with host_wait and compares every value
+__global__ void readback_pattern_kernel(double* out, int n, double base) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = base + (double)i;
+}
+int inf_debug_readback_check(int iters, int n, void* stream) {
+  if (iters < 0 || n <= 0 || n > (1 << 20)) return -INF_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  double* host = nullptr;
+  double* dev = nullptr;
+  hipEvent_t ev = nullptr;
+  int bad = 0, rc = INF_OK;
+  if (hipHostMalloc(reinterpret_cast<void**>(&host), sizeof(double) * n, hipHostMallocCoherent) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&dev), sizeof(double) * n) != hipSuccess ||
+      hipEventCreateWithFlags(&ev, INF_EV_SYNC) != hipSuccess) {
+    rc = INF_ERR_HIP;
+  }
+  const dim3 grid((n + 255) / 256), blk(256);
+  for (int r = 0; r < iters && rc == INF_OK; ++r) {
+    for (int form = 0; form < 2 && rc == INF_OK; ++form) {
+      const double base = 1e6 * (2 * r + form + 1);
+      if (form == 0) {
+        hipExtLaunchKernelGGL(readback_pattern_kernel, grid, blk, 0, s, nullptr, ev, 0, host, n, base);
+      } else {
+        hipLaunchKernelGGL(readback_pattern_kernel, grid, blk, 0, s, dev, n, base);
+        if (hipMemcpyAsync(host, dev, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(ev, s) != hipSuccess) rc = INF_ERR_HIP;
+      }
+      if (hipGetLastError() != hipSuccess) rc = INF_ERR_HIP;
+      if (rc == INF_OK) rc = host_wait(ev);
+      for (int i = 0; i < n && rc == INF_OK; ++i) bad += host[i] != base + (double)i;
+    }
+  }
+  (void)hipStreamSynchronize(s);
+  if (ev) (void)hipEventDestroy(ev);
+  if (dev) (void)hipFree(dev);
+  if (host) (void)hipHostFree(host);
+  return rc == INF_OK ? bad : -rc;
+}
+
 int inf_net_set_option(InfNet* n, int option, int value) {
   if (!n) return -INF_ERR_INVALID;
   int* slot = nullptr;

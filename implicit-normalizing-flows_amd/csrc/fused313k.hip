@@ -366,6 +366,21 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     }
   };
 
+  // the same for values already at the column scale: h = rne16(v), l = rne16(v - h) (v - h exact)
+  auto put_scaled = [&](int kt0, int b, const float (&v)[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const _Float16 h0 = (_Float16)v[4 * g], h1 = (_Float16)v[4 * g + 1], h2 = (_Float16)v[4 * g + 2], h3 = (_Float16)v[4 * g + 3];
+      const _Float16 l0 = (_Float16)(v[4 * g] - (float)h0), l1 = (_Float16)(v[4 * g + 1] - (float)h1);
+      const _Float16 l2 = (_Float16)(v[4 * g + 2] - (float)h2), l3 = (_Float16)(v[4 * g + 3] - (float)h3);
+      const f16x2 p0 = {h0, h1}, p1 = {h2, h3}, q0 = {l0, l1}, q1 = {l2, l3};
+      const int kt = kt0 + (g >> 1);
+      const int base = ((kt * KB_NB + b) * 2) * 64 + 32 * (g & 1) + li;
+      reinterpret_cast<uint2*>(cb + base)[lh] = make_uint2(__builtin_bit_cast(unsigned, p0), __builtin_bit_cast(unsigned, p1));
+      reinterpret_cast<uint2*>(cb + base + 64)[lh] = make_uint2(__builtin_bit_cast(unsigned, q0), __builtin_bit_cast(unsigned, q1));
+    }
+  };
+
   f32x16 acc[2][KB_NB];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -441,6 +456,28 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int b = b0 + g;
+        if constexpr (FAST && VJP) {
+          // the two power-of-two factors in one ldexp: vs = (acc d2) 2^(eA + sc) is (ldexp(acc, eA) d2) 2^sc bit for bit
+          // in the normal range, so no unscaled copy, no scale multiply in the check or the split; a column block whose
+          // max |vs| reaches fp16's range (inf too) sends the tile through the exact-scale path (a NaN yields NaN
+          // planes, as on that path)
+          const int es = eA + scB[b];
+          float vs[16];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 d = d2v[b][j];
+            vs[4 * j] = __builtin_amdgcn_ldexpf(ac[g][4 * j] * d.x, es);
+            vs[4 * j + 1] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 1] * d.y, es);
+            vs[4 * j + 2] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 2] * d.z, es);
+            vs[4 * j + 3] = __builtin_amdgcn_ldexpf(ac[g][4 * j + 3] * d.w, es);
+          }
+          float mx = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fabsf(vs[r]));
+          if (!(mx < 65504.f)) ovf[0] = 1;
+          put_scaled(2 * wid, b, vs);
+          continue;
+        }
         float cm = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

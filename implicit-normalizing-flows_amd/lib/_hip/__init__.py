@@ -142,6 +142,7 @@ _SIGS = {
     'inf_profile_end': (ctypes.c_int, [ctypes.POINTER(KernelStat), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     'inf_rademacher': (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P]),
     'inf_debug_poison_lds': (ctypes.c_int, [_P]),
+    'inf_debug_readback_check': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P]),
     'inf_net_set_option': (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
     'inf_net_get_option': (ctypes.c_int, [_P, ctypes.c_int]),
     'inf_banach_find_root': (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_double,

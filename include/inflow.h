@@ -374,6 +374,13 @@ int inf_net_surrogate_grad(InfNet* net, const float* x, const float* w, const fl
 /* ---- test support: fill the LDS of every CU with NaN (queued on `stream`), so a kernel that reads
  * LDS it never wrote fails deterministically instead of depending on what earlier kernels left. ---- */
 int inf_debug_poison_lds(void* stream);
+/* ---- test support: the readback contract.  The engine's host-read events (Broyden norm slots, the fc block kernel's
+ * statistics) are created without the system-scope fence (hipEventDisableSystemFence: a fenced event idles the GPU and
+ * cold-starts L2 after every readback); what the host reads behind them lives in coherent pinned memory that
+ * a kernel writes directly (the launch completing the event) or a D2H copy fills.  This runs `iters` rounds of both
+ * forms on `stream` with fresh values of n doubles each round, the host waiting exactly as the Broyden loop does, and
+ * returns the number of stale values the host saw (0 when the contract holds), or a negative status. ---- */
+int inf_debug_readback_check(int iters, int n, void* stream);
 
 /* Gradients of the log-det estimators of an fc net (the training path of train_tabular.py / train_toy.py: the basic
  * power series with create_graph, implicit_block.py:418-426; the brute-force log|det(I + J)|, :249-260; the exact-trace
