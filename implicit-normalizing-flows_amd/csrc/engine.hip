@@ -1292,16 +1292,21 @@ int broyden_solve(InfNet* f, const float* y, int B, int T, double eps_in, InfBro
   };
   const StartFn start = [&](float* x0, float* g0, float* upd, float* x1, float* dx) {
     first = false;
+    if (!f->fc)          // (conv: broyden_core's zero-copy per-sample sums are on whenever this start is passed)
+      return launch_broyden_start_sample(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, bf.stop_ev, &bf.stop_bound, upd,
+                                         x1, dx, B, f->d, s);
     return launch_broyden_start_fc(f->f0, bf.xemb, x0, g0, bf.fcur, bf.part, bf.stop_ev, &bf.stop_bound, upd, x1, dx,
                                    B, f->d, s);
   };
+  // conv nets: the one-launch start where the residual sums go straight into the readback slot (broyden_core zc)
+  const bool conv_start = !f->fc && SAMPLE_SUMS && out_nchunk(f->d) <= 4;
   if (f->line_search) {
     // line_search(on=True) (broyden.py:66-99): the global rule only (a per-sample step size is not the reference's)
     if (f->convergence != INF_CONV_GLOBAL) return INF_ERR_UNSUPPORTED;
     INF_TRY(broyden_core_ls(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true));
   } else {
     INF_TRY(broyden_core(f, resid, B, T, eps_in, stats, lowest_ss, bf, s, /*keep_f=*/true, f->fcfused ? &step : nullptr,
-                         f->fc ? &start : nullptr, tail, /*resid_sample_sums=*/true));
+                         (f->fc || conv_start) ? &start : nullptr, tail, /*resid_sample_sums=*/true));
   }
   if (diff_detail) {
     std::vector<float> dd(B);

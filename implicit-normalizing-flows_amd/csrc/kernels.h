@@ -148,6 +148,11 @@ int launch_sum_pairs(const float* gs, int T, int d, int batch, float* gx, hipStr
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s, int sample_sums = 0, hipEvent_t stop_ev = nullptr,
                        bool* stop_bound = nullptr);
+// conv layout, per-sample sums (d <= 4 OUT_CH chunks): x0 = 0, the residual at it, update = -g0, x1 = x0 + update,
+// dx = x1 - x0 in one launch, one block per sample, partial[b] the sample's sum of squares
+int launch_broyden_start_sample(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
+                                hipEvent_t stop_ev, bool* stop_bound, float* upd, float* x1, float* dx, int batch,
+                                int per, hipStream_t s);
 // fc layout (d, B): f0 holds d values
 int launch_resid_bcast_fc(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                           int batch, int d, hipStream_t s);

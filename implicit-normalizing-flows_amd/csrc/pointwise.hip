@@ -29,6 +29,26 @@ int out_nchunk(int per_sample) { return (per_sample + OUT_CH - 1) / OUT_CH; }
 //   OM_RECOMP: out0 = (fx - a) + x
 //   OM_VJP   : out0 = v = s (* swish'(x_in) for preact nets);  partial += v * eps
 // ------------------------------------------------------------------------------------------
+// The 9-tap sum at (c, p): every tap loaded from a clamped address (all nine in flight), the out-of-image ones then
+// added as +0 -- the same sum as adding only the in-image taps in tap order (s starts at +0 and never becomes -0, so
+// s + 0 == s): a bounds-checked load per tap made each thread wait nine times for memory
+__device__ __forceinline__ float tap_sum9(const float* yc, int P, int H, int W, int p) {
+  const int y = p / W, x = p - y * W;
+  float v[9];
+  bool ok[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+    ok[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int yc_ = min(max(yy, 0), H - 1), xc_ = min(max(xx, 0), W - 1);
+    v[t] = yc[(long)t * P + yc_ * W + xc_];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) s += ok[t] ? v[t] : 0.f;
+  return s;
+}
+
 template <int KS>
 __global__ __launch_bounds__(OUT_CH) void conv_out_kernel(OutArgs a) {
   __shared__ double red[16];
@@ -44,14 +64,7 @@ __global__ __launch_bounds__(OUT_CH) void conv_out_kernel(OutArgs a) {
     if constexpr (KS == 1) {
       s = a.Y[ybase + (long)c * P + p];
     } else {
-      const int y = p / a.W, x = p - y * a.W;
-      const float* yc = a.Y + ybase + (long)c * 9 * P;
-      s = 0.f;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) s += yc[(long)t * P + yy * a.W + xx];
-      }
+      s = tap_sum9(a.Y + ybase + (long)c * 9 * P, P, a.H, a.W, p);
     }
     const long ei = ebase + i;
     switch (a.mode) {
@@ -97,31 +110,32 @@ __global__ __launch_bounds__(OUT_CH) void conv_out_resid_sample_kernel(OutArgs a
   const int b = blockIdx.x;
   const int P = a.H * a.W, per = a.C * P;
   const long ybase = (long)b * a.y_sample, ebase = (long)b * per;
+  // every chunk's loads first (the element index clamped into the sample; out-of-sample elements are not stored and
+  // add nothing), then the epilogues
   double acc[NCH];
+  float sv[NCH], i0v[NCH], i1v[NCH], i2v[NCH];
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    const int i = min(cc * OUT_CH + (int)threadIdx.x, per - 1);
+    const int c = i / P, p = i - c * P;
+    if constexpr (KS == 1) sv[cc] = a.Y[ybase + (long)c * P + p];
+    else sv[cc] = tap_sum9(a.Y + ybase + (long)c * 9 * P, P, a.H, a.W, p);
+    const long ei = ebase + i;
+    i0v[cc] = a.in0[ei];
+    i1v[cc] = a.in1[ei];
+    i2v[cc] = a.in2 ? a.in2[ei] : 0.f;
+  }
 #pragma unroll
   for (int cc = 0; cc < NCH; ++cc) {
     acc[cc] = 0.0;
     const int i = cc * OUT_CH + threadIdx.x;
     if (i >= per) continue;
-    const int c = i / P, p = i - c * P;
-    float sv;
-    if constexpr (KS == 1) {
-      sv = a.Y[ybase + (long)c * P + p];
-    } else {
-      const int y = p / a.W, x = p - y * a.W;
-      const float* yc = a.Y + ybase + (long)c * 9 * P;
-      sv = 0.f;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) sv += yc[(long)t * P + yy * a.W + xx];
-      }
-    }
+    const int c = i / P;
     const long ei = ebase + i;
-    const float v = sv + a.bias[c];
-    const float gx = (a.in0[ei] - v) - a.in1[ei];
+    const float v = sv[cc] + a.bias[c];
+    const float gx = (i0v[cc] - v) - i1v[cc];
     a.out0[ei] = gx;
-    if (a.in2) a.out1[ei] = gx - a.in2[ei];
+    if (a.in2) a.out1[ei] = gx - i2v[cc];
     if (a.out2) a.out2[ei] = v;
     acc[cc] += (double)gx * (double)gx;
   }
@@ -219,6 +233,66 @@ __global__ __launch_bounds__(OUT_CH) void resid_bcast_sample_kernel(const float*
   }
   if (threadIdx.x == 0) partial[b] = tot;
 }
+// The conv root solve's start in one launch (global rule, per-sample sums into the readback slot): x0 = 0, the residual
+// at it from the cached f(0) (resid_bcast_sample_kernel's sums), update = -g0, x1 = x0 + update, dx = x1 - x0 -- the
+// memset, the residual, neg_kernel and axpy_step_kernel element for element (broyden_start_fc_kernel's conv form)
+template <int NCH>
+__global__ __launch_bounds__(OUT_CH) void broyden_start_sample_kernel(const float* f0, const float* xemb, float* x0,
+                                                                   float* g, float* fcur, double* partial, float* upd,
+                                                                   float* x1, float* dx, int per) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const long base = (long)b * per;
+  double acc[NCH];
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    acc[cc] = 0.0;
+    const int i = cc * OUT_CH + threadIdx.x;
+    if (i >= per) continue;
+    const long e = base + i;
+    const float z = 0.f;
+    const float v = f0[i];
+    const float gx = (xemb[e] - v) - z;
+    x0[e] = z;
+    g[e] = gx;
+    fcur[e] = v;
+    acc[cc] += (double)gx * (double)gx;
+    const float up = -gx;
+    upd[e] = up;
+    const float xe = z + up;
+    x1[e] = xe;
+    dx[e] = xe - z;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    const double t = block_sum(acc[cc], red);
+    tot += t;
+  }
+  if (threadIdx.x == 0) partial[b] = tot;
+}
+int launch_broyden_start_sample(const float* f0, const float* xemb, float* x0, float* g, float* fcur, double* partial,
+                                hipEvent_t stop_ev, bool* stop_bound, float* upd, float* x1, float* dx, int batch,
+                                int per, hipStream_t s) {
+  const int nch = out_nchunk(per);
+  const void* fn = nch == 1 ? reinterpret_cast<const void*>(&broyden_start_sample_kernel<1>)
+                 : nch == 2 ? reinterpret_cast<const void*>(&broyden_start_sample_kernel<2>)
+                 : nch == 3 ? reinterpret_cast<const void*>(&broyden_start_sample_kernel<3>)
+                 : nch == 4 ? reinterpret_cast<const void*>(&broyden_start_sample_kernel<4>) : nullptr;
+  if (!fn) return INF_ERR_INVALID;
+  void* args[] = {&f0, &xemb, &x0, &g, &fcur, &partial, &upd, &x1, &dx, &per};
+  const bool prof = prof_enabled();
+  if (stop_ev && !prof) {
+    INF_HIP(hipExtLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s, nullptr, stop_ev, 0));
+    if (stop_bound) *stop_bound = true;
+    return INF_OK;
+  }
+  if (prof) prof_begin_launch(s);
+  INF_HIP(hipLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s));
+  if (prof) prof_end_launch(s, 702, 0.0, 28.0 * batch * per + 4.0 * per);
+  return INF_OK;
+}
+
 int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float* g, float* fcur, double* partial,
                        int batch, int per, int nchunk, hipStream_t s, int sample_sums, hipEvent_t stop_ev,
                        bool* stop_bound) {
