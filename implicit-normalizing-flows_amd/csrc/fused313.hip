@@ -274,19 +274,33 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
       else pass(std::integral_constant<int, 1>(), i0);
     }
   } else {
-    for (int i = tid; i < vhz; i += NT) {
-      float v = 0.f;
-      if (i < vhn) {
-        const int c = i / (RH * CW), rr = i - c * RH * CW;
+    // FU elements per thread and pass, every load from a clamped address issued before any is used (a bounds-checked
+    // load per element waited for memory once per element: 6 round trips per thread at the 8x8 scale's 48 channels)
+    constexpr int FU = 8;
+    for (int i0 = tid; i0 < vhz; i0 += NT * FU) {
+      float lv[FU];
+      bool ok[FU];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int i = i0 + u * NT;
+        const int ic = i < vhn ? i : 0;
+        const int c = ic / (RH * CW), rr = ic - c * RH * CW;
         const int hy = rr / CW, hx = rr - hy * CW;
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-          v = in[(long)c * P + yy * a.W + xx];
+        ok[u] = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+        lv[u] = in[(long)c * P + min(max(yy, 0), a.H - 1) * a.W + min(max(xx, 0), a.W - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int i = i0 + u * NT;
+        float v = 0.f;
+        if (ok[u]) {
+          v = lv[u];
           if (a.pre_beta) v = swish_fast_f(v, pre_sp);
         }
+        if constexpr (H3AC) hmx = fmaxf(hmx, fabsf(v));
+        if (i < vhz) vh[i] = v;
       }
-      if constexpr (H3AC) hmx = fmaxf(hmx, fabsf(v));
-      vh[i] = v;
     }
   }
   // per-tile trace partial: wave sums -> a reserved LDS slot at the end of the LDS (never reused)

@@ -50,6 +50,9 @@ constexpr int KB_HID = 512;
 constexpr int KB_LDS = 40960;       // floats (160 KiB)
 constexpr int KB_CHUNK = 32768;     // floats: 16 K tiles x 4 column blocks x 2 planes x 64 lanes x 16 B
 constexpr int KB_TSLOTS = 32;
+#ifndef K128_D2EARLY
+#define K128_D2EARLY 0              // 1: chunk 1's first d2 loads issued in phase B's last K step instead of after phase B;
+#endif                              // measured neutral (16.83 / 16.89 vs 16.81 / 16.75 ms per step, same box; 9 spills)
 #ifndef K128_PSA
 #define K128_PSA 1                  // phase A's im2col planes split once per workgroup (0: per wave, A/B builds)
 #endif
@@ -259,19 +262,32 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       }
     } else {
       const float pre_sp = a.pre_beta ? softplus_f(ldc(a.pre_beta)) : 0.f;
-      for (int i = tid; i < vhz; i += KB_NT) {
-        float v = 0.f;
-        if (i < vhn) {
-          const int c = i / (RH * CW), rr = i - c * RH * CW;
+      // (as fused313.hip: every element's load from a clamped address issued before any is used)
+      constexpr int FU = 4;
+      for (int i0 = tid; i0 < vhz; i0 += KB_NT * FU) {
+        float lv[FU];
+        bool ok[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+          const int i = i0 + u * KB_NT;
+          const int ic = i < vhn ? i : 0;
+          const int c = ic / (RH * CW), rr = ic - c * RH * CW;
           const int hy = rr / CW, hx = rr - hy * CW;
           const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-          if (yy >= 0 && yy < a.H && xx >= 0 && xx < W) {
-            v = in[(long)c * P + yy * W + xx];
+          ok[u] = i < vhn && yy >= 0 && yy < a.H && xx >= 0 && xx < W;
+          lv[u] = in[(long)c * P + min(max(yy, 0), a.H - 1) * W + min(max(xx, 0), W - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+          const int i = i0 + u * KB_NT;
+          float v = 0.f;
+          if (ok[u]) {
+            v = lv[u];
             if (a.pre_beta) v = swish_fast_f(v, pre_sp);
           }
+          hmx = fmaxf(hmx, fabsf(v));
+          if (i < vhz) vh[i] = v;
         }
-        hmx = fmaxf(hmx, fabsf(v));
-        vh[i] = v;
       }
     }
   }
@@ -621,6 +637,14 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
             for (int k1 = 0; k1 < NKT1; ++k1) ldw2(A1h, (long)(8 + wid) * NKT1 + k1, lane, wA1[k1]);
           }
         }
+        if constexpr (c == 0 && K128_D2EARLY) {
+          // chunk 1's first two d2 column blocks behind them, so their HBM latency runs under the last two K steps'
+          // MFMAs (the remaining waits of the loop are for weight loads issued before: vmcnt retires in order)
+          if (kt == 14) {
+            loadD2(1, 0, 2);
+            __builtin_amdgcn_sched_barrier(0);         // (kept ahead of the step's MFMAs: the scheduler sank them)
+          }
+        }
         mmr(wa, hb, lb, kt + 1);
         if (kt + 2 < 16) ldW(kt + 2, wa);
         mmr(wb, hb, lb, min(kt + 2, 15));
@@ -629,7 +653,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
     if constexpr (c == 0) {
       KSTAMP(4);
       KSUB(0);
-      loadD2(1, 0, 2);
+      if constexpr (!K128_D2EARLY) loadD2(1, 0, 2);
     }
   };
   chunk(std::integral_constant<int, 0>());
