@@ -97,6 +97,18 @@ __device__ __forceinline__ f32x16 mma(const u32x4 (&a)[NP], const u32x4 (&b)[NP]
 #ifndef PS_C
 #define PS_C 1
 #endif
+// Wide kernel build options measured and not kept (round 6, one box, s2 VJP ms per step 2.56 / 2.52 with both vs 2.54 /
+// 2.45 without; stamps: staging 18.9 k and phase B 22.6 k clocks, unchanged): a 4-deep phase-B weight ring for the
+// per-wave split, and 6 halo elements per thread and pass of the series staging (the 48-channel halo in one pass)
+#ifndef WB_DEPTH
+#define WB_DEPTH 2   // wide kernel, per-wave split phase B: weight-fragment ring depth (K tiles)
+#endif
+#ifndef STAGE_WU
+#define STAGE_WU 4   // wide kernel: halo elements per thread and pass of the series staging
+#endif
+#ifndef PCD
+#define PCD 4        // pre-split wide kernel: phase C's weight-fragment ring depth for paired jobs (2: ping-pong)
+#endif
 #ifndef PSD
 #define PSD 4        // pre-split wide kernel: weight-fragment ring depth (K tiles) of phases A and B
 #endif
@@ -265,10 +277,14 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         if (i < vhz) vh[i] = v;
       }
     };
-    constexpr int SU = 4;
+    // (the wide variant has the registers for 6 units, 66 loads in flight: the 8x8 scale's 48-channel halo in one pass
+    // instead of two round trips)
+    constexpr int SU = (F_BN == 32 && F_LDS_FLOATS == LDS_FULL) ? STAGE_WU : 4;
     for (int i0 = tid; i0 < vhz; i0 += NT * SU) {
       const int nu = min(SU, (vhz - (i0 - tid) + NT - 1) / NT);     // wave-uniform
-      if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
+      if (SU >= 6 && nu >= 6) pass(std::integral_constant<int, (SU >= 6 ? 6 : 4)>(), i0);
+      else if (SU >= 5 && nu == 5) pass(std::integral_constant<int, (SU >= 5 ? 5 : 4)>(), i0);
+      else if (nu >= 4) pass(std::integral_constant<int, 4>(), i0);
       else if (nu == 3) pass(std::integral_constant<int, 3>(), i0);
       else if (nu == 2) pass(std::integral_constant<int, 2>(), i0);
       else pass(std::integral_constant<int, 1>(), i0);
@@ -697,12 +713,16 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
         }
       }
     } else {
-    constexpr int D = 2;
+    // weight-fragment ring: 2 K tiles (ping-pong); the wide variant (6 MFMAs per K step at NB = 1) WB_DEPTH
+    constexpr int D = (F_BN == 32 && F_LDS_FLOATS == LDS_FULL) ? WB_DEPTH : 2;
+    static_assert(nkt % D == 0, "phase-B K tiles must be a multiple of the ring depth");
     constexpr bool BPIPE = PB_BPIPE && F_LDS_FLOATS != LDS_HALF;
     u32x4 ab[D][TM][2];
     BOpH bo[BPIPE ? 2 : 1];
 #pragma unroll
-    for (int m = 0; m < TM; ++m) ld2(m, 0, ab[0][m]);
+    for (int d = 0; d + 1 < D; ++d)
+#pragma unroll
+      for (int m = 0; m < TM; ++m) ld2(m, d, ab[d][m]);
     if constexpr (BPIPE) bprep(0, bo[0]);
     for (int kt = 0; kt < nkt; kt += D) {
 #pragma unroll
@@ -1093,6 +1113,21 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
 #pragma unroll
             for (int g = 0; g < G; ++g) ld3(rbj[g], kt, o[g]);
           };
+          if (PCD > 2 && psc) {
+            // B operand from the planes (no VALU in the loop): the weight fragments PCD K tiles ahead, so the loop is not
+            // one L2 round trip per K tile (6 MFMAs per step at G = 2)
+            static_assert(PCD <= 2 || nkt % PCD == 0, "phase-C K tiles must be a multiple of the ring depth");
+            u32x4 rg[PCD > 2 ? PCD : 1][G][NPAC];
+#pragma unroll
+            for (int d = 0; d + 1 < PCD; ++d) ldg(d, rg[d]);
+            for (int kt = 0; kt < nkt; kt += PCD) {
+#pragma unroll
+              for (int d = 0; d < PCD; ++d) {
+                ldg(min(kt + d + PCD - 1, nkt - 1), rg[(d + PCD - 1) % PCD]);
+                step(kt + d, rg[d]);
+              }
+            }
+          } else {
           u32x4 p0[G][NPAC], q0[G][NPAC];
           ldg(0, p0);
           for (int kt = 0; kt < nkt; kt += 2) {
@@ -1100,6 +1135,7 @@ __device__ __forceinline__ void net313_body(const Net313Pair& pr) {
             step(kt, p0);
             if (kt + 2 < nkt) ldg(kt + 2, p0);
             step(kt + 1, q0);
+          }
           }
           if constexpr (H3AC) {
 #pragma unroll
