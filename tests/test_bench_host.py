@@ -54,17 +54,17 @@ def test_pending_pair_reads_every_batch():
 def test_roofline_phases_from_profile_stats():
     """roofline.phases (BASELINE.md:40-43's HBM-bound phases): per kernel the algorithmic GB/s of the profiling step's
     HIP-event times, and the committed rocprofv3 FETCH / WRITE traffic (profiles/pmc_phases.json) over the same time."""
-    stats = [dict(tag=711, launches=18, total_ms=0.1432, flops=0.0, bytes=18 * 4720128.0, peak_ms=0.0),
+    stats = [dict(tag=716, launches=18, total_ms=0.1432, flops=0.0, bytes=18 * 10223616.0, peak_ms=0.0),
              dict(tag=720, launches=12, total_ms=0.1191, flops=0.0, bytes=12 * 159488.0, peak_ms=0.0),
              dict(tag=532, launches=87, total_ms=16.2, flops=1e12, bytes=1e9, peak_ms=5.0)]
     ph = bench.hbm_phases(stats, 'cifar10', 64)
     assert set(ph) == {'broyden', 'hutchinson', 'basis'}
     p2 = ph['broyden']['kernels'][0]
-    assert p2['kernel'] == 'broyden_p2' and p2['launches'] == 18
-    assert abs(p2['GBs'] - 4720128.0 * 18 / 0.1432e-3 / 1e9) < 0.1
+    assert p2['kernel'] == 'broyden_fused_kernel' and p2['launches'] == 18
+    assert abs(p2['GBs'] - 10223616.0 * 18 / 0.1432e-3 / 1e9) < 0.1
     assert abs(p2['frac'] - p2['GBs'] / 8000.0) < 1e-4
-    # the committed PMC record for cifar10 at B = 64 carries broyden_p2 and series_combine_kernel
-    assert p2['traffic_per_launch'] > 0.9 * 4720128 and 'traffic_GBs' in ph['broyden']
+    # the committed PMC record for cifar10 at B = 64 (round 6) carries the fused Broyden update and series_combine_kernel
+    assert p2['traffic_per_launch'] > 0.5 * 10223616 and 'traffic_GBs' in ph['broyden']
     assert ph['hutchinson']['kernels'][0]['kernel'] == 'series_combine_kernel'
     assert 'pmc_phases.json[cifar10_b64]' in ph['basis']
     assert bench.hbm_phases(stats, 'cifar10', 63)['basis'].endswith('no PMC record')
