@@ -149,7 +149,8 @@ def parse():
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 # BASELINE.md's HBM-bound phases: the Broyden solve's update / residual kernels and the Hutchinson series' probe draw
 # and term combine (the probe dots themselves are fused into the VJP kernels' epilogues)
-PHASES = (('broyden', (700, 701, 702, 703, 704, 705, 706, 710, 711, 712, 713, 714, 715, 716)), ('hutchinson', (720, 721)))
+PHASES = (('broyden', (700, 701, 702, 703, 704, 705, 706, 708, 709, 710, 711, 712, 713, 714, 715, 716)),
+          ('hutchinson', (720, 721)))
 
 
 def hbm_phases(stats, config, batch):

@@ -289,7 +289,7 @@ int launch_broyden_start_sample(const float* f0, const float* xemb, float* x0, f
   }
   if (prof) prof_begin_launch(s);
   INF_HIP(hipLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s));
-  if (prof) prof_end_launch(s, 702, 0.0, 28.0 * batch * per + 4.0 * per);
+  if (prof) prof_end_launch(s, 708, 0.0, 28.0 * batch * per + 4.0 * per);
   return INF_OK;
 }
 
@@ -312,7 +312,7 @@ int launch_resid_bcast(const float* f0, const float* xemb, const float* z, float
     }
     if (prof) prof_begin_launch(s);
     INF_HIP(hipLaunchKernel(fn, dim3(batch), dim3(OUT_CH), args, 0, s));
-    if (prof) prof_end_launch(s, 700, 0.0, 16.0 * batch * per + 4.0 * per);
+    if (prof) prof_end_launch(s, 709, 0.0, 16.0 * batch * per + 4.0 * per);
     return INF_OK;
   }
   INF_PROF_LAUNCH(s, 700, 16.0 * batch * per + 4.0 * per, resid_bcast_kernel, dim3(out_nchunk(per), batch),

@@ -463,6 +463,7 @@ def profile_end():
 PHASE_TAGS = {
     700: 'resid_bcast_kernel', 701: 'resid_bcast_fc_kernel', 702: 'broyden_start_fc_kernel', 703: 'axpy_step_kernel',
     704: 'neg_kernel', 705: 'reduce_partials_kernel', 706: 'recomp_kernel', 707: 'line_step_kernel',
+    708: 'broyden_start_sample_kernel', 709: 'resid_bcast_sample_kernel',
     710: 'broyden_p1', 711: 'broyden_p2', 712: 'broyden_p3', 713: 'broyden_p4', 714: 'br_sum_chunks',
     715: 'broyden_small_d_kernel', 716: 'broyden_fused_kernel',
     720: 'series_combine_kernel', 721: 'rademacher_kernel',
