@@ -53,6 +53,9 @@ constexpr int KB_TSLOTS = 32;
 #ifndef K128_D2EARLY
 #define K128_D2EARLY 0              // 1: chunk 1's first d2 loads issued in phase B's last K step instead of after phase B;
 #endif                              // measured neutral (16.83 / 16.89 vs 16.81 / 16.75 ms per step, same box; 9 spills)
+#ifndef K128_PSA0
+#define K128_PSA0 1                 // chunk 0's im2col planes in the chunk buffer where they do not fit beside the halo
+#endif
 #ifndef K128_PSA
 #define K128_PSA 1                  // phase A's im2col planes split once per workgroup (0: per wave, A/B builds)
 #endif
@@ -343,8 +346,12 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
   constexpr int VH_OFF = KB_CHUNK + KB_NW * KB_BN + 8 + 2 * KB_NW + 4 + (9 * CT + 15) / 16 * 16;
   constexpr bool PSA = K128_PSA && CT > 0 && WT > 0 && VH_OFF + ((VHZc + 3) & ~3) + NKT1 * KB_NB * 512 <= KB_LDS;
   constexpr bool psa = PSA;           // (compile-time: a runtime switch costs the VJP 17 more spilled VGPRs)
-  u32x4* const pa = reinterpret_cast<u32x4*>(vh + ((vhz + 3) & ~3));
-  if constexpr (psa) {
+  // Where the planes do not fit beside the halo (the 12-channel scales: 56 KiB), chunk 0's phase A takes them from the
+  // chunk buffer, which its put only writes after the column-maxima barrier that ends phase A (K128_PSA0); chunk 1
+  // gathers and splits per wave as before
+  constexpr bool psa0 = K128_PSA0 && !PSA && CT > 0 && WT > 0 && NKT1 * KB_NB * 512 <= KB_CHUNK;
+  u32x4* const pa = psa0 ? cb : reinterpret_cast<u32x4*>(vh + ((vhz + 3) & ~3));
+  if constexpr (psa || psa0) {
     for (int s_ = tid; s_ < NKT1 * KB_NB * 64; s_ += KB_NT) {
       const int kt = s_ / (KB_NB * 64), rem = s_ - kt * (KB_NB * 64), b = rem >> 6, ln = rem & 63;
       const int n = b * 32 + (ln & 31), py = n / seg;
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(512) void net313k_kernel(Net313Pair pr) {
       constexpr bool PRE = c == 0 ? PRE_A0 : PRE_A1;
       if (!PRE) ldw2(A1h, (long)rbA * nkt1, lane, w0);
       auto stepA = [&](int kt, const u32x4 (&af)[2]) {
-        if constexpr (psa) {
+        if constexpr (psa || (psa0 && c == 0)) {
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             const u32x4 h = pa[((kt * KB_NB + b0 + g) * 2) * 64 + lane];

@@ -6,10 +6,10 @@ mkdir -p $O
 cd $R
 INFLOW_LIB=$R/altlib/lib_stamps.so timeout -k 10 120 python tools/series_only.py --scale 1 --mfma 2 --reps 2 --k128 1 > $O/s1.txt 2>&1 || exit 1
 grep -h "mode2\|pair" $O/s1.txt | cut -c1-330
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k "k128 or cifar or headline or split_bf16" > $O/tests.log 2>&1
+INFLOW_LIB=altlib/lib_psa0.so timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread -k "k128 or cifar or headline or split_bf16" > $O/tests.log 2>&1
 rc=$?; grep -E "passed|failed" $O/tests.log | tail -1; [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests.log | head; exit $rc; }
 i=0
-for cfg in "" "INFLOW_LIB=altlib/lib_nopsa0.so" "INFLOW_LIB=altlib/lib_psd2.so" "" "INFLOW_LIB=altlib/lib_nopsa0.so" "INFLOW_LIB=altlib/lib_psd2.so"; do
+for cfg in "" "INFLOW_LIB=altlib/lib_psa0.so" "INFLOW_LIB=altlib/lib_psd2.so" "" "INFLOW_LIB=altlib/lib_psa0.so" "INFLOW_LIB=altlib/lib_psd2.so"; do
   i=$((i+1))
   env $cfg timeout -k 10 300 python bench.py --cpu-baseline 0 --steps 60 --warmup 5 > $O/b$i.json 2> $O/b$i.err || { echo "bench [$cfg] failed"; tail $O/b$i.err; exit 1; }
   python - "$O/b$i.json" "$cfg" <<'PY'
