@@ -202,7 +202,16 @@ def ptr(t):
 
 
 def stream_of(t):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    """The raw HIP stream of the device's current torch stream (the per-call lookup, without a Stream object)."""
+    idx = t.device.index
+    return ctypes.c_void_p(_raw_stream(idx if idx is not None else torch.cuda.current_device()))
+
+
+def _raw_stream_slow(idx):
+    return torch.cuda.current_stream(idx).cuda_stream
+
+
+_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', _raw_stream_slow)
 
 
 def require_device(t, who):

@@ -25,6 +25,7 @@ nets for those two once-per-step pieces.
 """
 import copy
 import ctypes
+import math
 
 import numpy as np
 import torch
@@ -71,10 +72,10 @@ def set_convergence(mode):
 
 def _probes(shape, device):
     shard = _PROBES['shard']
-    per = int(np.prod(shape[1:]))
+    per = math.prod(shape[1:])
     if shard is None or shard[2] == shape[0] and shard[0] == 0:
         out = solvers.rademacher_probes(shape, device, _PROBES['mode'], _PROBES['seed'], _PROBES['offset'])
-        _PROBES['offset'] += int(np.prod(shape))
+        _PROBES['offset'] += math.prod(shape)
         return out
     lo, hi, n = shard
     if hi - lo != shape[0]:
@@ -572,7 +573,7 @@ class imBlock(nn.Module):
                 ests.append(_MemEffNeumannNative.apply(t, native, net, ws_pair[i], eps, *list(net.parameters())))
                 continue
             if not neumann and engine and t.dim() == 2:      # fc nets: the basic series with the graph, engine
-                co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+                co = solvers.logdet_coefficients(n_ps, coeff_fn)
                 ests.append(_LogdetFc.apply(t, native, net, netgrad.LOGDET_SERIES, eps, co,
                                             bool(self.training and self.grad_in_forward), *list(net.parameters())))
                 continue
@@ -724,7 +725,7 @@ class imBlock(nn.Module):
         plan = self._series_plan()
         n_ps, coeff_fn, ns = plan
         probes = (_probes(x.shape, x.device), _probes(x.shape, x.device))
-        co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+        co = solvers.logdet_coefficients(n_ps, coeff_fn)
         # the third region lets the engine run the x-branch series beside the root solve (inflow.h)
         ws = _hip.workspace(x.device, nx.ws_bytes(B, T) + nz.ws_bytes(B, 1) + nx.ws_bytes(B, 1))
         z = torch.empty_like(x)
@@ -832,7 +833,7 @@ class imBlock(nn.Module):
                                                   _hip.ptr(out[i]), B, _hip.ptr(ws), ws.numel(), stream),
                            'inf_logdet_neumann')
         else:
-            co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+            co = solvers.logdet_coefficients(n_ps, coeff_fn)
             carr = co.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
             # both branches in lockstep: one fused launch per series term for x- and z-nets
             ws = _hip.workspace(x.device, 2 * max(nx.ws_bytes(B), nz.ws_bytes(B)))

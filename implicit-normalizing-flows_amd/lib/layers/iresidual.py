@@ -157,7 +157,7 @@ class iResBlock(nn.Module):
                                               nco.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(out),
                                               B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_neumann')
         else:
-            co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+            co = solvers.logdet_coefficients(n_ps, coeff_fn)
             _hip.check(lib.inf_logdet_series(net.handle, _hip.ptr(x), _hip.ptr(vareps),
                                              co.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n_ps, _hip.ptr(out),
                                              B, _hip.ptr(ws), ws.numel(), stream), 'inf_logdet_series')

@@ -204,7 +204,25 @@ def series_coefficients(n_dist, p_or_lamb, n_exact, n_samples=1):
         raise ValueError('n_dist must be geometric or poisson')
     n_ps = int(max(ns)) + n_exact
     coeff_fn = lambda k: 1 / rcdf(k) * sum(ns >= k - n_exact) / len(ns)
+    coeff_fn.key = (n_dist, float(p_or_lamb), int(n_exact), tuple(int(v) for v in ns))   # the draw's outcome
     return n_ps, coeff_fn, ns
+
+
+_CO_CACHE = {}
+
+
+def logdet_coefficients(n_ps, coeff_fn):
+    """The series' log-det weights (-1)^(k+1)/k coeff_fn(k), k = 1..n_ps, as float32 (implicit_block.py:296-304).
+    Cached per draw outcome (coeff_fn.key, n_ps) so that a step does not re-evaluate the ~n_ps tail probabilities
+    in Python while the GPU waits at the block's start; the array is the same computation, read-only."""
+    key = getattr(coeff_fn, 'key', None)
+    co = _CO_CACHE.get((key, n_ps)) if key is not None else None
+    if co is None:
+        co = np.array([(-1) ** (k + 1) / k * coeff_fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+        if key is not None and len(_CO_CACHE) < 4096:
+            co.setflags(write=False)
+            _CO_CACHE[(key, n_ps)] = co
+    return co
 
 
 def exact_trace_logdet(net, x, n_ps, coeff_fn, stream):
