@@ -105,6 +105,23 @@ def test_series_coefficients_match_oracle(dist, param, n_exact):
         assert f1(k) == f2(k)
 
 
+@pytest.mark.parametrize('dist,param,n_exact,n_samples', [('poisson', 2.0, 20, 1), ('geometric', 0.5, 2, 1),
+                                                           ('poisson', 2.0, 10, 3)])
+def test_logdet_coefficients_cache_is_the_same_computation(dist, param, n_exact, n_samples):
+    """solvers.logdet_coefficients (the per-draw-outcome cache the eval path reads at a block's start) returns the
+    weights the uncached expression gives, bit for bit, for every draw outcome; the cached array is read-only."""
+    np.random.seed(7)
+    for _ in range(40):
+        n_ps, fn, ns = solvers.series_coefficients(dist, param, n_exact, n_samples)
+        want = np.array([(-1) ** (k + 1) / k * fn(k) for k in range(1, n_ps + 1)], dtype=np.float32)
+        for _rep in range(2):                           # the miss, then the hit
+            co = solvers.logdet_coefficients(n_ps, fn)
+            assert co.dtype == np.float32 and co.tobytes() == want.tobytes()
+            assert not co.flags.writeable
+    flat = solvers.logdet_coefficients(5, lambda k: 1.)  # training's fixed series (no draw): computed, not cached
+    assert flat.tobytes() == np.array([(-1) ** (k + 1) / k for k in range(1, 6)], dtype=np.float32).tobytes()
+
+
 def test_probe_replay_order_matches_reference_draw():
     torch.manual_seed(5)
     a = solvers.rademacher_probes((3, 4, 5), 'cpu', mode='reference')
